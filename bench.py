@@ -1,0 +1,209 @@
+"""Benchmark: FCE-YOLOv11 detection inference (forward + decode + NMS) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model yolo11n-fce.yaml] [--batch 32] [--imgsz 640]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+A step = one hipGraph replay of the whole forward over a resident synthetic batch
+(torch.rand(B,3,S,S) fp16, seeded per rank) + the device NMS of that batch.  Weights are the
+portable seeded weights of the named architecture (no checkpoints offline), broadcast from rank 0
+over RCCL.  Each rank owns its own batch shard (contiguous, reference ContiguousDistributedSampler
+rule); there is no data-path collective, so scaling is weak.  Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from collections import defaultdict
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import fce_pkg  # noqa: E402
+
+fce_pkg.load()
+from fce_yolo_amd.engine import NMS, Engine  # noqa: E402
+from fce_yolo_amd.parser import DetectionModel  # noqa: E402
+from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_F16_PEAK_TFS = 2500.0  # dense fp16 MFMA (no sparsity)
+RIDGE = MFMA_F16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+GFLOP_PER_IMG = {"yolo11n-fce": 6.338, "yolo11s-bifpn": 21.695, "yolo11m-fce": 263.13, "yolo11l-fce": 84.50}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="yolo11n-fce.yaml")
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--imgsz", type=int, default=640)
+    ap.add_argument("--no-nms", action="store_true", help="time the forward only")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
+    return ap.parse_args()
+
+
+def cpu_baseline(model_cfg: str, imgsz: int, seconds: float):
+    """The oracle (PyTorch-CPU fp32 restatement of the reference forward) on the host cores."""
+    from oracle import fce_oracle as O
+    from oracle.parse import parse
+
+    cpu_model = DetectionModel(model_cfg)
+    cpu_model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in cpu_model.state_dict().items()], 0))
+    layers, save, _ = parse(cpu_model.yaml)
+    sd = O.cast_sd(O.fuse_state_dict(cpu_model.state_dict()), torch.float32)
+    x = torch.rand(1, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(0))
+    with torch.inference_mode():
+        O.forward(layers, save, sd, x)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            O.forward(layers, save, sd, x)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 2000:
+                break
+    return {
+        "value": round(n / el, 3),
+        "unit": "images/sec",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"oracle fp32 forward of {model_cfg} @ {imgsz}x{imgsz}, bs=1, {n} images in {el:.1f} s "
+        f"(1 warm-up), torch {torch.__version__} CPU",
+    }
+
+
+def main():
+    a = parse_args()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != a.gpus:
+        a.gpus = world if world > 1 else a.gpus
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    model = DetectionModel(a.model)
+    if rank == 0:
+        model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
+    model.eval().to(dev)
+    if world > 1:  # weights broadcast once per model load (RCCL over xGMI)
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(t.data, src=0)
+
+    B, S = a.batch, a.imgsz
+    x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
+    eng = Engine(model, B, S, dev)
+    nms = NMS(B, eng.anchors, eng.nc, dev)
+
+    def step():
+        pred = eng(x)
+        if not a.no_nms:
+            nms(pred)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    ms_step = el / a.steps * 1e3
+    total_imgs = world * B * a.steps
+    value = total_imgs / el
+
+    # forward-only time (graph replay) for reference
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        eng(x)
+    barrier()
+    fwd_ms = (time.perf_counter() - t1) / a.steps * 1e3
+
+    # per-op HIP-event profile (eager, same kernels) -> dominant kernel family roofline
+    prof = eng.profile(x)
+    fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0])
+    for name, nbytes, flops, ms in prof:
+        f = fam[name]
+        f[0] += ms
+        f[1] += nbytes
+        f[2] += flops
+        f[3] += 1
+    dom = max(fam.items(), key=lambda kv: kv[1][0])
+    dname, (dms, dbytes, dflops, dn) = dom
+    ai = dflops / max(dbytes, 1.0)
+    if ai >= RIDGE:
+        ach = dflops / (dms / dn * 1e-3) / dn / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
+    else:
+        ach = dbytes / dn / (dms / dn * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = None
+    roof["kernel"] = dname
+    roof["launches_per_step"] = dn
+    roof["kernel_ms_per_step"] = round(dms, 4)
+    eager_ms = sum(p[3] for p in prof)
+    stem = Path(a.model).stem
+    gflop = GFLOP_PER_IMG.get(stem.replace("-h8", ""))
+    out = {
+        "metric": "images/sec/GPU @ 640x640 bs=32, yolo11n-fce; fraction of fp16 MFMA roofline",
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16",
+        "data": "synthetic torch.rand(B,3,S,S) fp16 per rank; seeded random-init weights of the architecture",
+        "config": {"workload": f"{stem} detection inference (forward + decode + NMS) @ {S}x{S}, {B} images/GPU",
+                   "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "forward_ms_per_batch": round(fwd_ms, 4),
+        "eager_sum_of_kernels_ms": round(eager_ms, 4),
+        "model_tflops": round(value / world * gflop / 1e3, 3) if gflop else None,
+        "kernels": {k: {"ms": round(v[0], 4), "launches": v[3], "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 1)
+                        if v[0] else None, "TFLOP/s": round(v[2] / (v[0] * 1e-3) / 1e12, 2) if v[0] else None}
+                    for k, v in sorted(fam.items(), key=lambda kv: -kv[1][0])},
+    }
+    if a.profile_json and rank == 0:
+        Path(a.profile_json).write_text(json.dumps([list(p) for p in prof], indent=0))
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

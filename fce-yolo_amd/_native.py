@@ -1,0 +1,152 @@
+"""ctypes binding of libfceyolo.so (the C-ABI declared in include/fce_yolo.h).
+
+The library is loaded from ``fce-yolo_amd/lib/libfceyolo.so`` (built in-tree by
+``build.py``).  Every wrapper raises ``FceError`` with ``fce_last_error()`` on a non-zero
+status; there is no fallback path: if the library is missing, ``lib()`` raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libfceyolo.so"
+
+F16, F32, U8 = 0, 1, 2
+NHWC, NCHW = 0, 1
+ACT_NONE, ACT_SILU = 0, 1
+EPI_STORE, EPI_WSTORE, EPI_ACCUM = 0, 1, 2
+
+
+class FceError(RuntimeError):
+    pass
+
+
+class Tensor(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p),
+        ("dtype", C.c_int),
+        ("layout", C.c_int),
+        ("n", C.c_int),
+        ("c", C.c_int),
+        ("h", C.c_int),
+        ("w", C.c_int),
+        ("cstride", C.c_int),
+        ("coff", C.c_int),
+    ]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("cin", C.c_int),
+        ("cout", C.c_int),
+        ("k", C.c_int),
+        ("stride", C.c_int),
+        ("groups", C.c_int),
+        ("act", C.c_int),
+        ("up", C.c_int),
+        ("epilogue", C.c_int),
+        ("fusion_w", C.c_void_p),
+        ("fusion_n", C.c_int),
+        ("fusion_i", C.c_int),
+    ]
+
+
+class CoordDesc(C.Structure):
+    _fields_ = [
+        ("inp", C.c_int),
+        ("oup", C.c_int),
+        ("mid", C.c_int),
+        ("heads", C.c_int),
+        ("scale", C.c_float),
+        ("w", C.c_void_p * 8),
+        ("b", C.c_void_p * 8),
+        ("id_w", C.c_void_p),
+        ("id_b", C.c_void_p),
+    ]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_SZ = C.c_size_t
+_PT = C.POINTER(Tensor)
+_PCD = C.POINTER(ConvDesc)
+_PCO = C.POINTER(CoordDesc)
+
+_SIGS = {
+    "fce_last_error": (C.c_char_p, []),
+    "fce_abi_version": (_I, []),
+    "fce_device_count": (_I, []),
+    "fce_conv_weight_bytes": (_SZ, [_PCD]),
+    "fce_conv_pack_weights": (_I, [_PCD, _P, _P]),
+    "fce_conv2d": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _P]),
+    "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),
+    "fce_weighted_add": (_I, [_PT, _I, _P, _I, _I, _I, _PT, _P]),
+    "fce_coord_workspace_bytes": (_SZ, [_PCO, _I, _I, _I]),
+    "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
+    "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
+    "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
+    "fce_psa_attention": (_I, [_PT, _I, _I, _I, _P, _P, _PT, _P]),
+    "fce_detect_decode": (_I, [_PT, _PT, _I, _P, _I, _P, _P]),
+    "fce_nms_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "fce_nms": (_I, [_P, _I, _I, _I, C.c_float, C.c_float, _I, _I, C.c_float, _P, _SZ, _P, _P, _P, _P]),
+    "fce_copy": (_I, [_PT, _PT, _P]),
+    "fce_net_create": (_P, []),
+    "fce_net_destroy": (None, [_P]),
+    "fce_net_add_buffer": (_I, [_P, _I, _I, _I]),
+    "fce_net_add_conv": (_I, [_P, _PCD, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "fce_net_add_maxpool_chain": (_I, [_P, _I, _I, _I, _I]),
+    "fce_net_add_weighted_add": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I]),
+    "fce_net_add_coord": (_I, [_P, _I, _PCO, _I, _I, _I, _I]),
+    "fce_net_add_psa_attention": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I]),
+    "fce_net_add_detect": (_I, [_P, _I, _P, _P, _I]),
+    "fce_net_plan": (_I, [_P, _I, _I, _I]),
+    "fce_net_arena_bytes": (_SZ, [_P]),
+    "fce_net_num_anchors": (_I, [_P]),
+    "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),
+    "fce_net_profile": (_I, [_P, _PT, _P, _P, _I, _P]),
+    "fce_net_num_ops": (_I, [_P]),
+    "fce_net_op_info": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "fce_net_buffer": (_I, [_P, _I, _PT]),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def lib():
+    """Load libfceyolo.so once.  Raises FceError if it has not been built."""
+    global _lib
+    if _lib is None:
+        path = Path(os.environ.get("FCE_YOLO_LIB", LIB_PATH))
+        if not path.exists():
+            raise FceError(f"libfceyolo.so not found at {path}: run `python fce-yolo_amd/build.py` (no fallback path)")
+        L = C.CDLL(str(path))
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = lib().fce_last_error().decode(errors="replace")
+        raise FceError(f"{what}: status {status}: {msg}")
+
+
+def call(name: str, *args):
+    st = getattr(lib(), name)(*args)
+    check(st, name)
+    return st
+
+
+def tensor(data_ptr: int, dtype: int, layout: int, n: int, c: int, h: int, w: int, cstride: int | None = None,
+           coff: int = 0) -> Tensor:
+    return Tensor(data_ptr, dtype, layout, n, c, h, w, c if cstride is None else cstride, coff)
+
+
+def ref(x):
+    return C.byref(x) if x is not None else None

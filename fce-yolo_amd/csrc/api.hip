@@ -1,0 +1,602 @@
+// C-ABI entry points (include/fce_yolo.h) and the native whole-graph executor.
+//
+// The executor restates BaseModel._predict_once (reference ultralytics/nn/tasks.py:160-188) as a
+// flat list of kernel launches over an NHWC fp16 arena whose buffers are planned once per
+// (batch, H, W): every layer output, every C2f/C3/SPPF/C2PSA concat buffer and the fp32 Detect
+// maps live at fixed offsets, so one forward is a fixed launch sequence that is captured into a
+// hipGraph and replayed (AutoBackend.forward / warmup, nn/autobackend.py:667-700, :912-926).
+#include <algorithm>
+#include <exception>
+#include <memory>
+#include <vector>
+
+#include "common.h"
+
+namespace fce {
+
+// kernels (other translation units)
+size_t conv_weight_bytes(const fce_conv_desc& d);
+int conv_pack(const fce_conv_desc& d, const float* w, void* out);
+int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
+           const fce_tensor& y, hipStream_t s);
+int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
+                  hipStream_t s);
+int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor& y,
+                 hipStream_t s);
+int copy(const fce_tensor& src, const fce_tensor& dst, hipStream_t s);
+size_t coord_ws_bytes(const fce_coord_desc& d, int n, int h, int w);
+int bicoordcrossatt(const fce_coord_desc& d, const fce_tensor& x, const fce_tensor& y, void* ws, size_t wsb,
+                    hipStream_t s);
+int coordatt(const fce_coord_desc& d, const fce_tensor& x, const fce_tensor& y, void* ws, size_t wsb, hipStream_t s);
+int coordcrossatt(const fce_coord_desc& d, const fce_tensor& x, const fce_tensor& y, void* ws, size_t wsb,
+                  hipStream_t s);
+int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, const float* pe_w, const float* pe_b,
+                  const fce_tensor& y, hipStream_t s);
+int detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
+                  float* out, hipStream_t s);
+size_t nms_ws_bytes(int n, int A, int max_nms);
+int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
+        void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
+
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+int fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+int check_nhwc(const fce_tensor* t, const char* name, int dtype) {
+  if (!t) return fail(FCE_ERR_INVALID, std::string(name) + ": null tensor");
+  if (t->layout != FCE_NHWC || t->dtype != dtype) return fail(FCE_ERR_INVALID, std::string(name) + ": wrong layout/dtype");
+  return FCE_OK;
+}
+
+}  // namespace fce
+
+using namespace fce;
+
+#define FCE_GUARD(body)                                    \
+  try {                                                    \
+    body                                                   \
+  } catch (const std::exception& e) {                      \
+    return fail(FCE_ERR_INVALID, std::string("exception: ") + e.what()); \
+  } catch (...) {                                          \
+    return fail(FCE_ERR_INVALID, "unknown exception");     \
+  }
+
+extern "C" {
+
+const char* fce_last_error(void) { return g_err.c_str(); }
+int fce_abi_version(void) { return FCE_ABI_VERSION; }
+int fce_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+size_t fce_conv_weight_bytes(const fce_conv_desc* d) { return d ? conv_weight_bytes(*d) : 0; }
+int fce_conv_pack_weights(const fce_conv_desc* d, const float* w, void* out) {
+  FCE_CHECK(d && w && out, "fce_conv_pack_weights: null argument");
+  FCE_GUARD(return conv_pack(*d, w, out);)
+}
+int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias, const fce_tensor* res,
+               const fce_tensor* y, void* stream) {
+  FCE_CHECK(d && x && w && bias && y, "fce_conv2d: null argument");
+  FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream));)
+}
+int fce_maxpool_chain(const fce_tensor* x, const fce_tensor* y1, const fce_tensor* y2, const fce_tensor* y3, int k,
+                      void* stream) {
+  FCE_CHECK(x && y1 && y2 && y3, "fce_maxpool_chain: null argument");
+  FCE_GUARD(return maxpool_chain(*x, *y1, *y2, *y3, k, S(stream));)
+}
+int fce_weighted_add(const fce_tensor* x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor* y,
+                     void* stream) {
+  FCE_CHECK(x && y, "fce_weighted_add: null argument");
+  FCE_GUARD(return weighted_add(*x, up, fw, fn, fi, accumulate, *y, S(stream));)
+}
+size_t fce_coord_workspace_bytes(const fce_coord_desc* d, int n, int h, int w) {
+  return d ? coord_ws_bytes(*d, n, h, w) : 0;
+}
+int fce_bicoordcrossatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t wsb,
+                        void* stream) {
+  FCE_CHECK(d && x && y, "fce_bicoordcrossatt: null argument");
+  FCE_GUARD(return bicoordcrossatt(*d, *x, *y, ws, wsb, S(stream));)
+}
+int fce_coordatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t wsb,
+                 void* stream) {
+  FCE_CHECK(d && x && y, "fce_coordatt: null argument");
+  FCE_GUARD(return coordatt(*d, *x, *y, ws, wsb, S(stream));)
+}
+int fce_coordcrossatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t wsb,
+                      void* stream) {
+  FCE_CHECK(d && x && y, "fce_coordcrossatt: null argument");
+  FCE_GUARD(return coordcrossatt(*d, *x, *y, ws, wsb, S(stream));)
+}
+int fce_psa_attention(const fce_tensor* qkv, int heads, int kd, int hd, const float* pe_w, const float* pe_b,
+                      const fce_tensor* y, void* stream) {
+  FCE_CHECK(qkv && y && pe_w && pe_b, "fce_psa_attention: null argument");
+  FCE_GUARD(return psa_attention(*qkv, heads, kd, hd, pe_w, pe_b, *y, S(stream));)
+}
+int fce_detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
+                      float* out, void* stream) {
+  FCE_CHECK(box && cls && strides && out, "fce_detect_decode: null argument");
+  FCE_GUARD(return detect_decode(box, cls, nl, strides, reg_max, out, S(stream));)
+}
+size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms) { return nms_ws_bytes(n, anchors, max_nms); }
+int fce_nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
+            void* ws, size_t wsb, float* dets, int64_t* keep, int32_t* counts, void* stream) {
+  FCE_CHECK(pred && dets && keep && counts, "fce_nms: null argument");
+  FCE_GUARD(return nms(pred, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts, S(stream));)
+}
+int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
+  FCE_CHECK(src && dst, "fce_copy: null argument");
+  FCE_GUARD(return copy(*src, *dst, S(stream));)
+}
+
+}  // extern "C"
+
+// ============================================================================ executor
+namespace {
+
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT };
+
+struct BufDesc {
+  int c, shift, dtype;
+  size_t offset = 0, bytes = 0;
+};
+
+struct OpDesc {
+  OpKind kind;
+  fce_conv_desc conv{};
+  fce_coord_desc coord{};
+  int coord_kind = 0;
+  int in = -1, in_coff = 0, in_c = 0;
+  int out = -1, out_coff = 0;
+  int res = -1, res_coff = 0;
+  const void* w = nullptr;
+  const float* b = nullptr;
+  int k = 0, up = 0, accumulate = 0;
+  const float* fw = nullptr;
+  int fn = 0, fi = 0;
+  int heads = 0, key_dim = 0, head_dim = 0;
+  const float* pe_w = nullptr;
+  const float* pe_b = nullptr;
+  int nl = 0;
+  int box[4] = {0, 0, 0, 0}, cls[4] = {0, 0, 0, 0};
+  float strides[4] = {0, 0, 0, 0};
+  int reg_max = 16;
+};
+
+}  // namespace
+
+struct fce_net {
+  std::vector<BufDesc> bufs;
+  std::vector<OpDesc> ops;
+  int batch = 0, H = 0, W = 0;
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  int anchors = 0, nc = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const void* cap_in = nullptr;
+  float* cap_out = nullptr;
+  hipStream_t cap_stream = nullptr;
+  fce_tensor cap_desc{};
+
+  void drop_graph() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    cap_in = nullptr;
+    cap_out = nullptr;
+  }
+  void release() {
+    drop_graph();
+    if (arena) (void)hipFree(arena);
+    if (ws) (void)hipFree(ws);
+    arena = nullptr;
+    ws = nullptr;
+    arena_bytes = ws_bytes = 0;
+  }
+  ~fce_net() { release(); }
+
+  fce_tensor view(int id, int coff, int c) const {
+    const BufDesc& b = bufs[id];
+    fce_tensor t{};
+    t.data = arena + b.offset;
+    t.dtype = b.dtype;
+    t.layout = FCE_NHWC;
+    t.n = batch;
+    t.c = c;
+    t.h = H >> b.shift;
+    t.w = W >> b.shift;
+    t.cstride = b.c;
+    t.coff = coff;
+    return t;
+  }
+};
+
+namespace {
+
+int op_input_view(const fce_net* net, const OpDesc& op, const fce_tensor& input, fce_tensor* out) {
+  if (op.in < 0) {
+    *out = input;
+    return FCE_OK;
+  }
+  *out = net->view(op.in, op.in_coff, op.in_c);
+  return FCE_OK;
+}
+
+int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred, hipStream_t s) {
+  fce_tensor x;
+  op_input_view(net, op, input, &x);
+  switch (op.kind) {
+    case OP_CONV: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.conv.cout);
+      fce_tensor r;
+      const fce_tensor* rp = nullptr;
+      if (op.res >= 0) {
+        r = net->view(op.res, op.res_coff, op.conv.cout);
+        rp = &r;
+      }
+      return conv2d(op.conv, x, op.w, op.b, rp, y, s);
+    }
+    case OP_MAXPOOL: {
+      const int c = op.in_c;
+      fce_tensor y1 = net->view(op.in, op.in_coff + c, c), y2 = net->view(op.in, op.in_coff + 2 * c, c),
+                 y3 = net->view(op.in, op.in_coff + 3 * c, c);
+      return maxpool_chain(x, y1, y2, y3, op.k, s);
+    }
+    case OP_WADD: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.in_c);
+      return weighted_add(x, op.up, op.fw, op.fn, op.fi, op.accumulate, y, s);
+    }
+    case OP_COORD: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.coord.oup);
+      if (op.coord_kind == 0) return bicoordcrossatt(op.coord, x, y, net->ws, net->ws_bytes, s);
+      if (op.coord_kind == 1) return coordatt(op.coord, x, y, net->ws, net->ws_bytes, s);
+      return coordcrossatt(op.coord, x, y, net->ws, net->ws_bytes, s);
+    }
+    case OP_PSA: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.heads * op.head_dim);
+      return psa_attention(x, op.heads, op.key_dim, op.head_dim, op.pe_w, op.pe_b, y, s);
+    }
+    case OP_DETECT: {
+      fce_tensor bx[4], cl[4];
+      for (int i = 0; i < op.nl; ++i) {
+        const int c = net->bufs[op.box[i]].c;
+        bx[i] = net->view(op.box[i], 0, 4 * op.reg_max);
+        cl[i] = net->view(op.cls[i], 4 * op.reg_max, c - 4 * op.reg_max);
+      }
+      return detect_decode(bx, cl, op.nl, op.strides, op.reg_max, pred, s);
+    }
+  }
+  return fail(FCE_ERR_INVALID, "unknown op");
+}
+
+int run_all(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s) {
+  for (const OpDesc& op : net->ops) {
+    int st = run_op(net, op, input, pred, s);
+    if (st) return st;
+  }
+  return FCE_OK;
+}
+
+void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* bytes, double* flops) {
+  const double N = net->batch;
+  auto hw = [&](int id) { return double(net->H >> net->bufs[id].shift) * double(net->W >> net->bufs[id].shift); };
+  *bytes = 0;
+  *flops = 0;
+  switch (op.kind) {
+    case OP_CONV: {
+      const fce_conv_desc& d = op.conv;
+      const double ohw = hw(op.out);
+      const double ihw = op.in >= 0 ? hw(op.in) : double(net->H) * net->W;
+      const int in_bytes = op.in >= 0 ? 2 : 2;  // f16 network input in the bench
+      const bool dw = d.groups > 1;
+      const bool stem = !dw && d.cin <= 4;
+      *name = stem ? "conv_stem" : dw ? "dwconv3x3" : (d.k == 3 ? "conv3x3_mfma" : "conv1x1_mfma");
+      const int osz = net->bufs[op.out].dtype == FCE_F32 ? 4 : 2;
+      *bytes = N * ihw * d.cin * in_bytes + N * ohw * d.cout * osz + double(conv_weight_bytes(d));
+      if (op.res >= 0) *bytes += N * ohw * d.cout * 2;
+      if (d.epilogue == FCE_EPI_ACCUM) *bytes += N * ohw * d.cout * 2;
+      *flops = 2.0 * N * ohw * d.cout * d.k * d.k * (dw ? 1 : d.cin);
+      break;
+    }
+    case OP_MAXPOOL:
+      *name = "maxpool_chain";
+      *bytes = N * hw(op.in) * op.in_c * 2 * 4;
+      break;
+    case OP_WADD:
+      *name = "bifpn_weighted_add";
+      *bytes = N * hw(op.out) * op.in_c * 2 * (op.accumulate ? 3 : 2) / (op.up ? 1.6 : 1.0);
+      break;
+    case OP_COORD: {
+      const char* nm[3] = {"bicoordcrossatt", "coordatt", "coordcrossatt"};
+      *name = nm[op.coord_kind];
+      const double px = N * hw(op.in);
+      *bytes = px * op.coord.inp * 2 * 2 + px * op.coord.oup * 2;  // 2 reads (pool, gate) + 1 write
+      const double L = double(net->H >> net->bufs[op.in].shift) + double(net->W >> net->bufs[op.in].shift);
+      *flops = 2.0 * N * (3.0 * op.coord.mid * op.coord.inp * L + op.coord.oup * op.coord.mid * L);
+      break;
+    }
+    case OP_PSA: {
+      *name = "psa_attention";
+      const double t = hw(op.in);
+      *bytes = N * t * op.heads * (2 * op.key_dim + op.head_dim) * 2 + N * t * op.heads * op.head_dim * 2;
+      *flops = 2.0 * N * op.heads * t * t * (op.key_dim + op.head_dim);
+      break;
+    }
+    case OP_DETECT: {
+      *name = "detect_decode";
+      double a = 0;
+      for (int i = 0; i < op.nl; ++i) a += hw(op.box[i]);
+      *bytes = N * a * (4 * op.reg_max + net->nc) * 4 + N * a * (4 + net->nc) * 4;
+      break;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+fce_net* fce_net_create(void) {
+  try {
+    return new fce_net();
+  } catch (...) {
+    set_error("fce_net_create: allocation failed");
+    return nullptr;
+  }
+}
+void fce_net_destroy(fce_net* net) { delete net; }
+
+int fce_net_add_buffer(fce_net* net, int c, int shift, int dtype) {
+  FCE_CHECK(net && c > 0 && shift >= 0 && shift <= 8 && (dtype == FCE_F16 || dtype == FCE_F32),
+            "fce_net_add_buffer: bad argument");
+  net->drop_graph();
+  net->bufs.push_back(BufDesc{c, shift, dtype});
+  return int(net->bufs.size()) - 1;
+}
+
+static int valid_buf(const fce_net* net, int id, bool allow_input) {
+  return (allow_input && id == -1) || (id >= 0 && id < int(net->bufs.size()));
+}
+
+int fce_net_add_conv(fce_net* net, const fce_conv_desc* d, int in, int in_coff, int out, int out_coff, int res,
+                     int res_coff, const void* w, const float* b) {
+  FCE_CHECK(net && d && w && b, "fce_net_add_conv: null argument");
+  FCE_CHECK(valid_buf(net, in, true) && valid_buf(net, out, false) && (res == -1 || valid_buf(net, res, false)),
+            "fce_net_add_conv: bad buffer id");
+  OpDesc op;
+  op.kind = OP_CONV;
+  op.conv = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->cin;
+  op.out = out;
+  op.out_coff = out_coff;
+  op.res = res;
+  op.res_coff = res_coff;
+  op.w = w;
+  op.b = b;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_maxpool_chain(fce_net* net, int buf, int in_coff, int c, int k) {
+  FCE_CHECK(net && valid_buf(net, buf, false), "fce_net_add_maxpool_chain: bad buffer");
+  OpDesc op;
+  op.kind = OP_MAXPOOL;
+  op.in = buf;
+  op.in_coff = in_coff;
+  op.in_c = c;
+  op.k = k;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_weighted_add(fce_net* net, int in, int in_coff, int c, int up, const float* fw, int fn, int fi,
+                             int accumulate, int out, int out_coff) {
+  FCE_CHECK(net && fw && valid_buf(net, in, false) && valid_buf(net, out, false), "fce_net_add_weighted_add: bad arg");
+  OpDesc op;
+  op.kind = OP_WADD;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = c;
+  op.up = up;
+  op.fw = fw;
+  op.fn = fn;
+  op.fi = fi;
+  op.accumulate = accumulate;
+  op.out = out;
+  op.out_coff = out_coff;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_coord(fce_net* net, int kind, const fce_coord_desc* d, int in, int in_coff, int out, int out_coff) {
+  FCE_CHECK(net && d && kind >= 0 && kind <= 2 && valid_buf(net, in, false) && valid_buf(net, out, false),
+            "fce_net_add_coord: bad argument");
+  OpDesc op;
+  op.kind = OP_COORD;
+  op.coord_kind = kind;
+  op.coord = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->inp;
+  op.out = out;
+  op.out_coff = out_coff;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_psa_attention(fce_net* net, int qkv, int heads, int kd, int hd, const float* pe_w, const float* pe_b,
+                              int out, int out_coff) {
+  FCE_CHECK(net && pe_w && pe_b && valid_buf(net, qkv, false) && valid_buf(net, out, false),
+            "fce_net_add_psa_attention: bad argument");
+  OpDesc op;
+  op.kind = OP_PSA;
+  op.in = qkv;
+  op.in_coff = 0;
+  op.in_c = heads * (2 * kd + hd);
+  op.heads = heads;
+  op.key_dim = kd;
+  op.head_dim = hd;
+  op.pe_w = pe_w;
+  op.pe_b = pe_b;
+  op.out = out;
+  op.out_coff = out_coff;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_detect(fce_net* net, int nl, const int* maps, const float* strides, int reg_max) {
+  FCE_CHECK(net && maps && strides && nl >= 1 && nl <= 4, "fce_net_add_detect: bad argument");
+  OpDesc op;
+  op.kind = OP_DETECT;
+  op.nl = nl;
+  for (int i = 0; i < nl; ++i) {
+    FCE_CHECK(valid_buf(net, maps[i], false), "fce_net_add_detect: bad buffer");
+    FCE_CHECK(net->bufs[maps[i]].dtype == FCE_F32 && net->bufs[maps[i]].c > 4 * reg_max, "detect maps must be f32");
+    op.box[i] = maps[i];
+    op.cls[i] = maps[i];
+    op.strides[i] = strides[i];
+  }
+  op.in = maps[0];
+  op.reg_max = reg_max;
+  net->nc = net->bufs[maps[0]].c - 4 * reg_max;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_plan(fce_net* net, int batch, int h, int w) {
+  FCE_CHECK(net && batch > 0 && h > 0 && w > 0, "fce_net_plan: bad argument");
+  FCE_CHECK(h % 32 == 0 && w % 32 == 0, "fce_net_plan: H and W must be multiples of 32 (max stride)");
+  FCE_GUARD({
+    net->release();
+    net->batch = batch;
+    net->H = h;
+    net->W = w;
+    size_t off = 0;
+    for (BufDesc& b : net->bufs) {
+      b.offset = off;
+      b.bytes = size_t(batch) * (h >> b.shift) * (w >> b.shift) * b.c * dtype_size(b.dtype);
+      off += (b.bytes + 255) & ~size_t(255);
+    }
+    net->arena_bytes = off;
+    size_t ws = 256;
+    int A = 0;
+    for (const OpDesc& op : net->ops) {
+      if (op.kind == OP_COORD)
+        ws = std::max(ws, coord_ws_bytes(op.coord, batch, h >> net->bufs[op.in].shift, w >> net->bufs[op.in].shift));
+      if (op.kind == OP_DETECT)
+        for (int i = 0; i < op.nl; ++i) A += (h >> net->bufs[op.box[i]].shift) * (w >> net->bufs[op.box[i]].shift);
+    }
+    net->anchors = A;
+    net->ws_bytes = ws;
+    FCE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&net->arena), std::max<size_t>(off, 256)));
+    FCE_HIP_CHECK(hipMalloc(&net->ws, ws));
+    FCE_HIP_CHECK(hipMemset(net->arena, 0, std::max<size_t>(off, 256)));
+    return FCE_OK;
+  })
+}
+
+size_t fce_net_arena_bytes(const fce_net* net) { return net ? net->arena_bytes + net->ws_bytes : 0; }
+int fce_net_num_anchors(const fce_net* net) { return net ? net->anchors : 0; }
+int fce_net_num_ops(const fce_net* net) { return net ? int(net->ops.size()) : 0; }
+
+static int check_input(const fce_net* net, const fce_tensor* in) {
+  FCE_CHECK(net->arena, "fce_net: call fce_net_plan first");
+  FCE_CHECK(in && in->layout == FCE_NCHW && in->n == net->batch && in->h == net->H && in->w == net->W,
+            "fce_net: input must be NCHW with the planned batch/size");
+  return FCE_OK;
+}
+
+int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int graph, void* stream) {
+  FCE_CHECK(net && pred, "fce_net_forward: null argument");
+  int st = check_input(net, input);
+  if (st) return st;
+  hipStream_t s = S(stream);
+  FCE_GUARD({
+    if (!graph || s == nullptr) return run_all(net, *input, pred, s);
+    const bool same = net->exec && net->cap_in == input->data && net->cap_out == pred && net->cap_stream == s &&
+                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c;
+    if (!same) {
+      net->drop_graph();
+      FCE_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      st = run_all(net, *input, pred, s);
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamEndCapture(s, &g);
+      if (st) {
+        if (g) (void)hipGraphDestroy(g);
+        return st;
+      }
+      FCE_HIP_CHECK(e);
+      net->graph = g;
+      FCE_HIP_CHECK(hipGraphInstantiate(&net->exec, g, nullptr, nullptr, 0));
+      net->cap_in = input->data;
+      net->cap_out = pred;
+      net->cap_stream = s;
+      net->cap_desc = *input;
+    }
+    FCE_HIP_CHECK(hipGraphLaunch(net->exec, s));
+    return FCE_OK;
+  })
+}
+
+int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int cap, void* stream) {
+  FCE_CHECK(net && pred && ms, "fce_net_profile: null argument");
+  int st = check_input(net, input);
+  if (st) return st;
+  hipStream_t s = S(stream);
+  FCE_GUARD({
+    const int nops = int(net->ops.size());
+    std::vector<hipEvent_t> ev(nops + 1);
+    for (auto& e : ev) FCE_HIP_CHECK(hipEventCreate(&e));
+    FCE_HIP_CHECK(hipEventRecord(ev[0], s));
+    for (int i = 0; i < nops; ++i) {
+      st = run_op(net, net->ops[i], *input, pred, s);
+      if (st) break;
+      FCE_HIP_CHECK(hipEventRecord(ev[i + 1], s));
+    }
+    if (!st) {
+      FCE_HIP_CHECK(hipEventSynchronize(ev[nops]));
+      for (int i = 0; i < nops && i < cap; ++i) FCE_HIP_CHECK(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return st;
+  })
+}
+
+int fce_net_op_info(const fce_net* net, int i, char* name, int cap, double* bytes, double* flops) {
+  FCE_CHECK(net && i >= 0 && i < int(net->ops.size()) && bytes && flops, "fce_net_op_info: bad argument");
+  FCE_CHECK(net->batch > 0, "fce_net_op_info: plan first");
+  std::string nm;
+  op_cost(net, net->ops[i], &nm, bytes, flops);
+  if (name && cap > 0) {
+    size_t n = std::min(nm.size(), size_t(cap - 1));
+    nm.copy(name, n);
+    name[n] = 0;
+  }
+  return FCE_OK;
+}
+
+int fce_net_buffer(const fce_net* net, int id, fce_tensor* out) {
+  FCE_CHECK(net && out && id >= 0 && id < int(net->bufs.size()) && net->arena, "fce_net_buffer: bad argument");
+  *out = net->view(id, 0, net->bufs[id].c);
+  return FCE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,64 @@
+// Shared helpers for the gfx950 kernels and the C-ABI glue.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/fce_yolo.h"
+
+namespace fce {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- error state (thread-local)
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define FCE_HIP_CHECK(expr)                                                                    \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return ::fce::fail(FCE_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+#define FCE_CHECK(cond, msg)                                           \
+  do {                                                                 \
+    if (!(cond)) return ::fce::fail(FCE_ERR_INVALID, std::string(msg)); \
+  } while (0)
+
+inline int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FCE_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return FCE_OK;
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- device math
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// BiFPN normalised weight (fce_block.py:57-58): relu(w_i) / (sum_j relu(w_j) + 1e-4)
+__device__ __forceinline__ float fusion_alpha(const float* w, int n, int i) {
+  float s = 0.f;
+  for (int j = 0; j < n; ++j) s += fmaxf(w[j], 0.f);
+  return fmaxf(w[i], 0.f) / (s + 1e-4f);
+}
+
+// NHWC element offset of pixel (n,y,x) channel c in a view
+__host__ __device__ __forceinline__ int64_t nhwc_off(int n, int y, int x, int H, int W, int cstride) {
+  return ((int64_t(n) * H + y) * W + x) * cstride;
+}
+
+inline int64_t numel(const fce_tensor& t) { return int64_t(t.n) * t.c * t.h * t.w; }
+inline int dtype_size(int dt) { return dt == FCE_F32 ? 4 : dt == FCE_U8 ? 1 : 2; }
+
+int check_nhwc(const fce_tensor* t, const char* name, int dtype);
+
+}  // namespace fce

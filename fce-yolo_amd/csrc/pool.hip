@@ -1,0 +1,195 @@
+// SPPF max-pool chain, BiFPN identity-branch fusion and layout/dtype edge copies (NHWC fp16).
+//
+// maxpool_chain replaces block.py:228-232: y1 = mp5(x), y2 = mp5(y1), y3 = mp5(y2) with
+// MaxPool2d(5, 1, 2) (-inf padding, Q13).  A chain of k x k stride-1 max pools with -inf padding
+// equals one (2k-1) / (3k-2) window pool over the clamped window (max is associative and every
+// in-range element of the larger window is reachable through an in-range intermediate), so all
+// three outputs come from one read of x and are written straight into the concat buffer slices.
+#include "common.h"
+
+namespace fce {
+
+struct MpArgs {
+  const _Float16* x;
+  int xcs;
+  _Float16* y1;
+  _Float16* y2;
+  _Float16* y3;
+  int y1cs, y2cs, y3cs;
+  int N, H, W, C, r;  // r = k/2
+};
+
+__global__ __launch_bounds__(256) void maxpool_chain_kernel(MpArgs a) {
+  const int cg = a.C / 8;
+  const int64_t total = int64_t(a.N) * a.H * a.W * cg;
+  const int R3 = 3 * a.r;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int g = int(t % cg);
+    const int64_t pix = t / cg;
+    const int ox = int(pix % a.W), oy = int((pix / a.W) % a.H), n = int(pix / (int64_t(a.W) * a.H));
+    float m1[8], m2[8], m3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m1[j] = m2[j] = m3[j] = -INFINITY;
+    for (int dy = -R3; dy <= R3; ++dy) {
+      const int iy = oy + dy;
+      if (iy < 0 || iy >= a.H) continue;
+      const int ady = dy < 0 ? -dy : dy;
+      float r1[8], r2[8], r3[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r1[j] = r2[j] = r3[j] = -INFINITY;
+      for (int dx = -R3; dx <= R3; ++dx) {
+        const int ix = ox + dx;
+        if (ix < 0 || ix >= a.W) continue;
+        const int adx = dx < 0 ? -dx : dx;
+        const h8 v = *reinterpret_cast<const h8*>(a.x + nhwc_off(n, iy, ix, a.H, a.W, a.xcs) + g * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)v[j];
+          r3[j] = fmaxf(r3[j], f);
+          if (adx <= 2 * a.r) r2[j] = fmaxf(r2[j], f);
+          if (adx <= a.r) r1[j] = fmaxf(r1[j], f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        m3[j] = fmaxf(m3[j], r3[j]);
+        if (ady <= 2 * a.r) m2[j] = fmaxf(m2[j], r2[j]);
+        if (ady <= a.r) m1[j] = fmaxf(m1[j], r1[j]);
+      }
+    }
+    h8 o1, o2, o3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = (_Float16)m1[j];
+      o2[j] = (_Float16)m2[j];
+      o3[j] = (_Float16)m3[j];
+    }
+    *reinterpret_cast<h8*>(a.y1 + pix * a.y1cs + g * 8) = o1;
+    *reinterpret_cast<h8*>(a.y2 + pix * a.y2cs + g * 8) = o2;
+    *reinterpret_cast<h8*>(a.y3 + pix * a.y3cs + g * 8) = o3;
+  }
+}
+
+int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
+                  hipStream_t s) {
+  for (const fce_tensor* t : {&x, &y1, &y2, &y3}) {
+    FCE_CHECK(t->layout == FCE_NHWC && t->dtype == FCE_F16, "maxpool_chain: NHWC f16 views");
+    FCE_CHECK(t->cstride % 8 == 0 && t->coff % 8 == 0, "maxpool_chain: 8-channel aligned slices");
+    FCE_CHECK(t->n == x.n && t->c == x.c && t->h == x.h && t->w == x.w, "maxpool_chain: shape mismatch");
+  }
+  FCE_CHECK(x.c % 8 == 0 && (k & 1), "maxpool_chain: c % 8 == 0, odd k");
+  MpArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.cstride,
+           static_cast<_Float16*>(y1.data) + y1.coff, static_cast<_Float16*>(y2.data) + y2.coff,
+           static_cast<_Float16*>(y3.data) + y3.coff, y1.cstride, y2.cstride, y3.cstride,
+           x.n, x.h, x.w, x.c, k / 2};
+  const int64_t total = int64_t(x.n) * x.h * x.w * (x.c / 8);
+  if (total == 0) return FCE_OK;
+  int blocks = int(std::min<int64_t>((total + 255) / 256, 65535 * 8));
+  hipLaunchKernelGGL(maxpool_chain_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return launch_status("maxpool_chain_kernel");
+}
+
+// ---------------------------------------------------------------------------- BiFPN identity term
+struct WaddArgs {
+  const _Float16* x;
+  int xcs, Hs, Ws, up;
+  _Float16* y;
+  int ycs, N, H, W, C;
+  const float* fw;
+  int fn, fi, accumulate;
+};
+
+__global__ __launch_bounds__(256) void weighted_add_kernel(WaddArgs a) {
+  const float alpha = fusion_alpha(a.fw, a.fn, a.fi);
+  const int cg = a.C / 8;
+  const int64_t total = int64_t(a.N) * a.H * a.W * cg;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int g = int(t % cg);
+    const int64_t pix = t / cg;
+    const int ox = int(pix % a.W), oy = int((pix / a.W) % a.H), n = int(pix / (int64_t(a.W) * a.H));
+    const h8 v = *reinterpret_cast<const h8*>(a.x + nhwc_off(n, oy >> a.up, ox >> a.up, a.Hs, a.Ws, a.xcs) + g * 8);
+    _Float16* yo = a.y + pix * a.ycs + g * 8;
+    h8 prev = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (a.accumulate) prev = *reinterpret_cast<const h8*>(yo);
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)((a.accumulate ? (float)prev[j] : 0.f) + alpha * (float)v[j]);
+    *reinterpret_cast<h8*>(yo) = o;
+  }
+}
+
+int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor& y,
+                 hipStream_t s) {
+  FCE_CHECK(x.layout == FCE_NHWC && y.layout == FCE_NHWC && x.dtype == FCE_F16 && y.dtype == FCE_F16,
+            "weighted_add: NHWC f16 views");
+  FCE_CHECK(x.c == y.c && x.n == y.n && (x.h << up) == y.h && (x.w << up) == y.w, "weighted_add: shape mismatch");
+  FCE_CHECK(x.c % 8 == 0 && x.cstride % 8 == 0 && x.coff % 8 == 0 && y.cstride % 8 == 0 && y.coff % 8 == 0,
+            "weighted_add: 8-channel aligned slices");
+  FCE_CHECK(fw && fn > fi && fi >= 0, "weighted_add: fusion weights");
+  WaddArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.cstride, x.h, x.w, up,
+             static_cast<_Float16*>(y.data) + y.coff, y.cstride, y.n, y.h, y.w, y.c, fw, fn, fi, accumulate};
+  const int64_t total = int64_t(y.n) * y.h * y.w * (y.c / 8);
+  if (total == 0) return FCE_OK;
+  hipLaunchKernelGGL(weighted_add_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256),
+                     0, s, a);
+  return launch_status("weighted_add_kernel");
+}
+
+// ---------------------------------------------------------------------------- layout / dtype copies
+struct CopyArgs {
+  const void* src;
+  int sdt, slay, scs, scoff;
+  void* dst;
+  int ddt, dlay, dcs, dcoff;
+  int N, C, H, W;
+};
+
+__device__ __forceinline__ int64_t view_index(int lay, int cs, int coff, int n, int c, int y, int x, int C, int H,
+                                              int W) {
+  return lay == FCE_NCHW ? ((int64_t(n) * C + c) * H + y) * W + x : ((int64_t(n) * H + y) * W + x) * cs + coff + c;
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
+  const int64_t total = int64_t(a.N) * a.C * a.H * a.W;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    // iterate in destination order for coalesced stores
+    int n, c, y, x;
+    if (a.dlay == FCE_NCHW) {
+      x = int(t % a.W);
+      y = int((t / a.W) % a.H);
+      c = int((t / (int64_t(a.W) * a.H)) % a.C);
+      n = int(t / (int64_t(a.W) * a.H * a.C));
+    } else {
+      c = int(t % a.C);
+      x = int((t / a.C) % a.W);
+      y = int((t / (int64_t(a.C) * a.W)) % a.H);
+      n = int(t / (int64_t(a.C) * a.W * a.H));
+    }
+    const int64_t si = view_index(a.slay, a.scs, a.scoff, n, c, y, x, a.C, a.H, a.W);
+    const int64_t di = view_index(a.dlay, a.dcs, a.dcoff, n, c, y, x, a.C, a.H, a.W);
+    float v;
+    if (a.sdt == FCE_F16)
+      v = (float)static_cast<const _Float16*>(a.src)[si];
+    else if (a.sdt == FCE_F32)
+      v = static_cast<const float*>(a.src)[si];
+    else
+      v = (float)static_cast<const uint8_t*>(a.src)[si];
+    if (a.ddt == FCE_F16)
+      static_cast<_Float16*>(a.dst)[di] = (_Float16)v;
+    else
+      static_cast<float*>(a.dst)[di] = v;
+  }
+}
+
+int copy(const fce_tensor& src, const fce_tensor& dst, hipStream_t s) {
+  FCE_CHECK(src.n == dst.n && src.c == dst.c && src.h == dst.h && src.w == dst.w, "copy: shape mismatch");
+  FCE_CHECK(dst.dtype == FCE_F16 || dst.dtype == FCE_F32, "copy: destination must be f16 or f32");
+  const int64_t total = numel(src);
+  if (total == 0) return FCE_OK;
+  CopyArgs a{src.data, src.dtype, src.layout, src.cstride, src.coff, dst.data, dst.dtype,
+             dst.layout, dst.cstride, dst.coff, src.n, src.c, src.h, src.w};
+  hipLaunchKernelGGL(copy_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256), 0, s, a);
+  return launch_status("copy_kernel");
+}
+
+}  // namespace fce

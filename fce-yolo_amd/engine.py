@@ -1,0 +1,129 @@
+"""Whole-graph inference engine and NMS (the AutoBackend / predictor side of the path).
+
+``Engine`` lowers a ``DetectionModel`` once into a native ``fce_net`` (buffer arena + launch list),
+plans it for (batch, H, W) and runs it as one hipGraph replay per batch — the MI355X form of
+``AutoBackend.forward`` (reference ``nn/autobackend.py:667-700``) + ``_predict_once``
+(``nn/tasks.py:160-188``).  ``non_max_suppression`` runs the device NMS kernel with the predict
+defaults of ``utils/nms.py:13-166`` / ``cfg/default.yaml:53-55`` (conf 0.25, iou 0.7, max_det 300,
+max_nms 30000, max_wh 7680) and returns the same per-image (k, 6) tensors and kept anchor indices.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as N
+from .backend import NetBackend
+
+_DT = {torch.float16: N.F16, torch.float32: N.F32, torch.uint8: N.U8}
+
+
+class Engine:
+    def __init__(self, model, batch: int, imgsz: int | tuple[int, int], device=None, graph: bool = True):
+        if isinstance(imgsz, int):
+            imgsz = (imgsz, imgsz)
+        self.H, self.W = imgsz
+        self.batch = batch
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        if self.device.type != "cuda":
+            raise RuntimeError("Engine: fce_yolo_amd runs on ROCm devices only; no CPU fallback")
+        self.model = model
+        self.graph = graph
+        self.be = NetBackend(self.H, self.W, self.device)
+        with torch.no_grad():
+            x = self.be.input_view(batch, model.yaml.get("channels", 3))
+            model.emit(self.be, x)
+        N.call("fce_net_plan", self.be.net, batch, self.H, self.W)
+        self.anchors = N.lib().fce_net_num_anchors(self.be.net)
+        self.nc = model.model[-1].nc
+        self.pred = torch.empty((batch, 4 + self.nc, self.anchors), dtype=torch.float32, device=self.device)
+
+    def close(self):
+        self.be.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def net(self):
+        return self.be.net
+
+    def _in(self, x: torch.Tensor) -> N.Tensor:
+        if x.device != self.device or x.dtype not in _DT:
+            raise ValueError("Engine: input must be f16/f32/u8 on the engine's device")
+        if tuple(x.shape) != (self.batch, 3, self.H, self.W) or not x.is_contiguous():
+            raise ValueError(f"Engine: input must be contiguous NCHW {(self.batch, 3, self.H, self.W)}")
+        return N.Tensor(x.data_ptr(), _DT[x.dtype], N.NCHW, self.batch, 3, self.H, self.W, 3, 0)
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, graph: bool | None = None) -> torch.Tensor:
+        out = self.pred if out is None else out
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        g = self.graph if graph is None else graph
+        N.call("fce_net_forward", self.be.net, C.byref(self._in(x)), out.data_ptr(), int(bool(g)), stream)
+        return out
+
+    def profile(self, x: torch.Tensor):
+        """Eager run with a hipEvent pair around every op: [(name, ms, bytes, flops)]."""
+        n = N.lib().fce_net_num_ops(self.be.net)
+        ms = (C.c_float * n)()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        N.call("fce_net_profile", self.be.net, C.byref(self._in(x)), self.pred.data_ptr(), C.cast(ms, C.c_void_p), n,
+               stream)
+        return [(*self.op_info(i), float(ms[i])) for i in range(n)]
+
+    def op_info(self, i: int):
+        name = C.create_string_buffer(64)
+        b, f = C.c_double(), C.c_double()
+        N.call("fce_net_op_info", self.be.net, i, name, 64, C.byref(b), C.byref(f))
+        return name.value.decode(), b.value, f.value
+
+    def num_ops(self) -> int:
+        return N.lib().fce_net_num_ops(self.be.net)
+
+    def arena_bytes(self) -> int:
+        return N.lib().fce_net_arena_bytes(self.be.net)
+
+
+class NMS:
+    """Device NMS with persistent workspace/outputs (graph-capturable)."""
+
+    def __init__(self, batch, anchors, nc, device, conf=0.25, iou=0.7, max_det=300, max_nms=30000, max_wh=7680):
+        self.batch, self.anchors, self.nc = batch, anchors, nc
+        self.conf, self.iou, self.max_det, self.max_nms, self.max_wh = conf, iou, max_det, max_nms, max_wh
+        nb = N.lib().fce_nms_workspace_bytes(batch, anchors, max_nms)
+        self.ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
+        self.dets = torch.zeros((batch, max_det, 6), dtype=torch.float32, device=device)
+        self.keep = torch.zeros((batch, max_det), dtype=torch.int64, device=device)
+        self.counts = torch.zeros((batch,), dtype=torch.int32, device=device)
+        self.device = device
+
+    def __call__(self, pred: torch.Tensor):
+        assert pred.is_contiguous() and pred.dtype == torch.float32 and tuple(pred.shape) == (
+            self.batch, 4 + self.nc, self.anchors)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        N.call("fce_nms", pred.data_ptr(), self.batch, self.nc, self.anchors, self.conf, self.iou, self.max_det,
+               self.max_nms, float(self.max_wh), self.ws.data_ptr(), self.ws.numel(), self.dets.data_ptr(),
+               self.keep.data_ptr(), self.counts.data_ptr(), stream)
+        return self.dets, self.keep, self.counts
+
+    def results(self):
+        counts = self.counts.cpu().tolist()
+        return ([self.dets[b, :k] for b, k in enumerate(counts)], [self.keep[b, :k] for b, k in enumerate(counts)])
+
+
+def non_max_suppression(pred: torch.Tensor, conf_thres=0.25, iou_thres=0.7, max_det=300, max_nms=30000, max_wh=7680,
+                        return_idxs=False):
+    """nms.py:13-166 on the device: list of (k, 6) [x1,y1,x2,y2,conf,cls] per image (+ kept anchor indices)."""
+    if pred.device.type != "cuda":
+        raise RuntimeError("non_max_suppression: ROCm device tensor required (no CPU fallback)")
+    pred = pred.float().contiguous()
+    b, no, a = pred.shape
+    nms = NMS(b, a, no - 4, pred.device, conf_thres, iou_thres, max_det, max_nms, max_wh)
+    nms(pred)
+    dets, keep = nms.results()
+    return (dets, keep) if return_idxs else dets

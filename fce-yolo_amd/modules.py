@@ -1,0 +1,651 @@
+"""Drop-in nn.Modules for the FCE-YOLOv11 inference path.
+
+Each class has the reference's name, constructor signature and state_dict layout (key names,
+shapes and registration order), so ``yolo11-fce.yaml`` builds through a ``parse_model`` that
+resolves module names to these classes (reference ``ultralytics/nn/tasks.py:1582-1588``) and
+reference checkpoints' state_dicts load unchanged.  ``forward`` runs the HIP kernels through the
+C-ABI (eager drop-in mode, NCHW-logical / NHWC-physical channels_last tensors); ``emit`` lowers the
+same computation onto a backend (see ``backend.py``), which is how the whole-graph executor is
+built.  There is no CPU path: a CPU tensor raises.
+
+BatchNorm eps is 1e-3 (reference ``utils/torch_utils.py:470`` sets it for every model; Q4), and
+BN is folded into the conv at first use exactly like ``fuse_conv_and_bn`` (torch_utils.py:237-267).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .backend import EagerBackend, View
+
+BN_EPS = 1e-3
+
+__all__ = (
+    "Conv", "DWConv", "Bottleneck", "C2f", "C3", "C3k", "C3k2", "SPPF", "Attention", "PSABlock", "C2PSA",
+    "Concat", "Upsample", "BiFPN_Concat", "CoordAtt", "CoordCrossAtt", "BiCoordCrossAtt", "DFL", "Detect",
+)
+
+
+def autopad(k, p=None, d=1):
+    """conv.py:30-36."""
+    if d > 1:
+        k = d * (k - 1) + 1 if isinstance(k, int) else [d * (x - 1) + 1 for x in k]
+    if p is None:
+        p = k // 2 if isinstance(k, int) else [x // 2 for x in k]
+    return p
+
+
+# ============================================================================ native weight cache
+def _state_key(mod: nn.Module, device):
+    ts = list(mod.parameters()) + list(mod.buffers())
+    return (str(device),) + tuple((t.data_ptr(), t._version, t.dtype) for t in ts)
+
+
+def _cached(mod: nn.Module, device, build, slot: str = "_fce_native"):
+    """Native (folded / packed / fp32) copies of a module's weights, rebuilt when any of its
+    tensors changes (data_ptr / version counter / dtype) or the device differs."""
+    key = _state_key(mod, device)
+    c = mod.__dict__.get(slot)
+    if c is None or c[0] != key:
+        c = (key, build())
+        mod.__dict__[slot] = c
+    return c[1]
+
+
+def fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d | None):
+    """fp32 (w, b) with BN folded (torch_utils.py:237-267)."""
+    with torch.no_grad():
+        w = conv.weight.detach().float()
+        b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(w.shape[0], device=w.device)
+        if bn is not None:
+            g, beta = bn.weight.detach().float(), bn.bias.detach().float()
+            mean, var = bn.running_mean.detach().float(), bn.running_var.detach().float()
+            s = g / torch.sqrt(bn.eps + var)
+            w = (w.view(w.shape[0], -1) * s[:, None]).view(w.shape)
+            b = s * b + (beta - g * mean / torch.sqrt(var + bn.eps))
+    return w, b
+
+
+def pack_conv(desc: N.ConvDesc, w: torch.Tensor, device) -> torch.Tensor:
+    """Pack an OIHW fp32 weight into the kernel's image (C-ABI fce_conv_pack_weights) on `device`."""
+    wh = np.ascontiguousarray(w.detach().float().cpu().numpy())
+    nb = N.lib().fce_conv_weight_bytes(C.byref(desc))
+    out = np.empty(nb, dtype=np.uint8)
+    N.call("fce_conv_pack_weights", C.byref(desc), wh.ctypes.data, out.ctypes.data)
+    return torch.from_numpy(out).to(device)
+
+
+class _ConvNative:
+    __slots__ = ("desc", "w", "b")
+
+    def __init__(self, desc, w, b):
+        self.desc, self.w, self.b = desc, w, b
+
+
+def conv_native(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, act: bool, device) -> _ConvNative:
+    def build():
+        if conv.dilation != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
+            raise NotImplementedError("fce_yolo_amd: dilated / non-square convs are not on the YOLO11 path")
+        k = conv.kernel_size[0]
+        if conv.padding != (k // 2, k // 2):
+            raise NotImplementedError("fce_yolo_amd: only 'same' (k//2) padding")
+        w, b = fold_bn(conv, bn)
+        g = conv.groups
+        desc = N.ConvDesc(conv.in_channels, conv.out_channels, k, conv.stride[0], g, N.ACT_SILU if act else N.ACT_NONE,
+                          0, N.EPI_STORE, None, 0, 0)
+        if g not in (1, conv.in_channels) or (g > 1 and conv.in_channels != conv.out_channels):
+            raise NotImplementedError("fce_yolo_amd: grouped convs other than depthwise")
+        return _ConvNative(desc, pack_conv(desc, w, device), b.to(device).contiguous())
+
+    # cached on the conv module; the key covers the conv's and the BN's tensors
+    ts = list(conv.parameters()) + list(conv.buffers()) + (list(bn.parameters()) + list(bn.buffers()) if bn else [])
+    key = (str(device), act) + tuple((t.data_ptr(), t._version, t.dtype) for t in ts)
+    c = conv.__dict__.get("_fce_conv")
+    if c is None or c[0] != key:
+        c = (key, build())
+        conv.__dict__["_fce_conv"] = c
+    return c[1]
+
+
+def _desc_copy(d: N.ConvDesc, **kw) -> N.ConvDesc:
+    n = N.ConvDesc()
+    C.pointer(n)[0] = d
+    for k, v in kw.items():
+        setattr(n, k, v)
+    return n
+
+
+def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = None, res: View | None = None,
+              epilogue: int = N.EPI_STORE, fusion=None, out_dtype=N.F16) -> View:
+    nat = conv_native(conv, bn, act, be.device)
+    k, s = conv.kernel_size[0], conv.stride[0]
+    ho = (x.h + 2 * (k // 2) - k) // s + 1
+    wo = (x.w + 2 * (k // 2) - k) // s + 1
+    y = out if out is not None else be.alloc(x.n, conv.out_channels, ho, wo, out_dtype)
+    assert (y.h, y.w, y.c) == (ho, wo, conv.out_channels), "output view mismatch"
+    fw, fn, fi = fusion if fusion is not None else (None, 0, 0)
+    desc = _desc_copy(nat.desc, epilogue=epilogue, fusion_w=fw, fusion_n=fn, fusion_i=fi)
+    if x.layout == N.NCHW and conv.in_channels > 4:
+        x = be.from_torch(x.buf) if isinstance(be, EagerBackend) else x
+    if x.up and (k != 1 or conv.groups != 1):
+        x = be.materialize(x)
+    be.conv(desc, x, y, nat.w.data_ptr(), nat.b.data_ptr(), res)
+    return y
+
+
+def _run_eager(mod, x, *, keep_nchw=False, out_dtype=None):
+    """Drop-in forward: NCHW tensor(s) in, channels_last tensor out (input dtype preserved)."""
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    dev = xs[0].device
+    if dev.type != "cuda":
+        raise RuntimeError(f"{type(mod).__name__}: fce_yolo_amd runs on ROCm devices only (got {dev}); no CPU fallback")
+    be = EagerBackend(dev)
+    views = [be.from_torch(t, keep_nchw=keep_nchw) for t in xs]
+    y = mod.emit(be, views if isinstance(x, (list, tuple)) else views[0])
+    dt = out_dtype or xs[0].dtype
+    if dt not in (torch.float16, torch.float32):
+        dt = torch.float16
+    return be.to_torch(y, dt)
+
+
+# ============================================================================ conv.py
+class Conv(nn.Module):
+    """conv.py:39-89: SiLU(BN(conv(x)))."""
+
+    default_act = nn.SiLU()
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, c2, k, s, autopad(k, p, d), groups=g, dilation=d, bias=False)
+        self.bn = nn.BatchNorm2d(c2, eps=BN_EPS)
+        self.act = self.default_act if act is True else act if isinstance(act, nn.Module) else nn.Identity()
+
+    def _act(self) -> bool:
+        if isinstance(self.act, nn.SiLU):
+            return True
+        if isinstance(self.act, nn.Identity):
+            return False
+        raise NotImplementedError(f"fce_yolo_amd: activation {type(self.act).__name__} is not on the YOLO11 path")
+
+    def emit(self, be, x, out=None, res=None, epilogue=N.EPI_STORE, fusion=None, out_dtype=N.F16):
+        return emit_conv(be, self.conv, getattr(self, "bn", None), self._act(), x, out, res, epilogue, fusion,
+                         out_dtype)
+
+    def forward(self, x):
+        return _run_eager(self, x, keep_nchw=self.conv.in_channels <= 4)
+
+    def forward_fuse(self, x):
+        return self.forward(x)
+
+
+class DWConv(Conv):
+    """conv.py:185-200."""
+
+    def __init__(self, c1, c2, k=1, s=1, d=1, act=True):
+        super().__init__(c1, c2, k, s, g=math.gcd(c1, c2), d=d, act=act)
+
+
+class Concat(nn.Module):
+    """conv.py:616-641: torch.cat along channels as channel-offset copies into one buffer."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def emit(self, be, xs, out=None):
+        assert self.d == 1
+        c = sum(v.c for v in xs)
+        y = out if out is not None else be.alloc(xs[0].n, c, xs[0].h, xs[0].w)
+        off = 0
+        for v in xs:
+            be.wadd(v, y.slice(off, v.c), None, 0)
+            off += v.c
+        return y
+
+    def forward(self, x):
+        return _run_eager(self, list(x))
+
+
+class Upsample(nn.Upsample):
+    """nn.Upsample(None, 2, 'nearest') fused into the consumer's loads (lazy view)."""
+
+    def emit(self, be, x, out=None):
+        if self.mode != "nearest" or float(self.scale_factor) != 2.0:
+            raise NotImplementedError("fce_yolo_amd: only nearest x2 upsampling")
+        v = x.upsampled(2)
+        return v if out is None else be.wadd(v, out, None, 0) or out
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+# ============================================================================ block.py
+class Bottleneck(nn.Module):
+    """block.py:452-476."""
+
+    def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, k[0], 1)
+        self.cv2 = Conv(c_, c2, k[1], 1, g=g)
+        self.add = shortcut and c1 == c2
+
+    def emit(self, be, x, out=None):
+        h = self.cv1.emit(be, x)
+        return self.cv2.emit(be, h, out=out, res=x if self.add else None)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class C2f(nn.Module):
+    """block.py:270-315: cv1 -> chunk(2) -> n blocks -> cat -> cv2; the cat is one buffer."""
+
+    def __init__(self, c1, c2, n=1, shortcut=False, g=1, e=0.5):
+        super().__init__()
+        self.c = int(c2 * e)
+        self.cv1 = Conv(c1, 2 * self.c, 1, 1)
+        self.cv2 = Conv((2 + n) * self.c, c2, 1)
+        self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
+
+    def emit(self, be, x, out=None):
+        c, n = self.c, len(self.m)
+        buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
+        self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
+        for i, m in enumerate(self.m):
+            m.emit(be, buf.slice((1 + i) * c, c), out=buf.slice((2 + i) * c, c))
+        return self.cv2.emit(be, buf, out=out)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class C3(nn.Module):
+    """block.py:318-340."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c1, c_, 1, 1)
+        self.cv3 = Conv(2 * c_, c2, 1)
+        self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, k=((1, 1), (3, 3)), e=1.0) for _ in range(n)))
+
+    def emit(self, be, x, out=None):
+        c_ = self.cv1.conv.out_channels
+        buf = be.alloc(x.n, 2 * c_, x.h, x.w)
+        a = self.cv1.emit(be, x) if len(self.m) else self.cv1.emit(be, x, out=buf.slice(0, c_))
+        for i, m in enumerate(self.m):
+            a = m.emit(be, a, out=buf.slice(0, c_) if i == len(self.m) - 1 else None)
+        self.cv2.emit(be, x, out=buf.slice(c_, c_))
+        return self.cv3.emit(be, buf, out=out)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class C3k(C3):
+    """block.py:1087-1108."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5, k=3):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, k=(k, k), e=1.0) for _ in range(n)))
+
+
+class C3k2(C2f):
+    """block.py:1064-1084."""
+
+    def __init__(self, c1, c2, n=1, c3k=False, e=0.5, g=1, shortcut=True):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        self.m = nn.ModuleList(
+            C3k(self.c, self.c, 2, shortcut, g) if c3k else Bottleneck(self.c, self.c, shortcut, g) for _ in range(n)
+        )
+
+
+class SPPF(nn.Module):
+    """block.py:205-232; the three chained MaxPool2d(5,1,2) run as one kernel into the concat buffer."""
+
+    def __init__(self, c1, c2, k=5):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_ * 4, c2, 1, 1)
+        self.m = nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2)
+
+    def emit(self, be, x, out=None):
+        c_ = self.cv1.conv.out_channels
+        buf = be.alloc(x.n, 4 * c_, x.h, x.w)
+        self.cv1.emit(be, x, out=buf.slice(0, c_))
+        be.maxpool_chain(buf, c_, self.m.kernel_size if isinstance(self.m.kernel_size, int) else self.m.kernel_size[0])
+        return self.cv2.emit(be, buf, out=out)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class Attention(nn.Module):
+    """block.py:1247-1304."""
+
+    def __init__(self, dim, num_heads=8, attn_ratio=0.5):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.key_dim = int(self.head_dim * attn_ratio)
+        self.scale = self.key_dim**-0.5
+        nh_kd = self.key_dim * num_heads
+        h = dim + nh_kd * 2
+        self.qkv = Conv(dim, h, 1, act=False)
+        self.proj = Conv(dim, dim, 1, act=False)
+        self.pe = Conv(dim, dim, 3, 1, g=dim, act=False)
+
+    def _pe(self, device):
+        def build():
+            w, b = fold_bn(self.pe.conv, getattr(self.pe, "bn", None))
+            return w.reshape(w.shape[0], 9).contiguous().to(device), b.contiguous().to(device)
+
+        return _cached(self.pe, device, build, "_fce_pe")
+
+    def emit(self, be, x, out=None, res=None):
+        qkv = self.qkv.emit(be, x)
+        o = be.alloc(x.n, self.num_heads * self.head_dim, x.h, x.w)
+        pw, pb = self._pe(be.device)
+        be.psa(qkv, self.num_heads, self.key_dim, self.head_dim, pw.data_ptr(), pb.data_ptr(), o)
+        return self.proj.emit(be, o, out=out, res=res)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class PSABlock(nn.Module):
+    """block.py:1307-1354."""
+
+    def __init__(self, c, attn_ratio=0.5, num_heads=4, shortcut=True):
+        super().__init__()
+        self.attn = Attention(c, attn_ratio=attn_ratio, num_heads=num_heads)
+        self.ffn = nn.Sequential(Conv(c, c * 2, 1), Conv(c * 2, c, 1, act=False))
+        self.add = shortcut
+
+    def emit(self, be, x, out=None):
+        x1 = self.attn.emit(be, x, res=x if self.add else None)
+        f = self.ffn[0].emit(be, x1)
+        return self.ffn[1].emit(be, f, out=out, res=x1 if self.add else None)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class C2PSA(nn.Module):
+    """block.py:1412-1464."""
+
+    def __init__(self, c1, c2, n=1, e=0.5):
+        super().__init__()
+        assert c1 == c2
+        self.c = int(c1 * e)
+        self.cv1 = Conv(c1, 2 * self.c, 1, 1)
+        self.cv2 = Conv(2 * self.c, c1, 1)
+        self.m = nn.Sequential(*(PSABlock(self.c, attn_ratio=0.5, num_heads=self.c // 64) for _ in range(n)))
+
+    def emit(self, be, x, out=None):
+        c = self.c
+        buf = self.cv1.emit(be, x)  # [a | b]
+        b = buf.slice(c, c)
+        for i, m in enumerate(self.m):
+            b = m.emit(be, b, out=buf.slice(c, c) if i == len(self.m) - 1 else None)
+        return self.cv2.emit(be, buf, out=out)
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+# ============================================================================ fce_block.py
+class BiFPN_Concat(nn.Module):
+    """fce_block.py:13-63: sum_i relu(w_i)/(sum relu(w)+1e-4) * realign_i(x_i).
+
+    Realign convs run with a weighted-store / accumulate epilogue into one output buffer; Identity
+    branches (and upsampled inputs) use the weighted-add kernel; the normalised weights are
+    computed on the device from ``w`` so a captured graph needs no host round trip."""
+
+    def __init__(self, c1, c2=None):
+        super().__init__()
+        self.output_ch = c2 if c2 else max(c1)
+        self.realign_convs = nn.ModuleList()
+        for ch in c1:
+            if ch != self.output_ch:
+                self.realign_convs.append(Conv(ch, self.output_ch, 1, 1))
+            else:
+                self.realign_convs.append(nn.Identity())
+        self.w = nn.Parameter(torch.ones(len(c1), dtype=torch.float32), requires_grad=True)
+        self.epsilon = 1e-4
+
+    def _w32(self, device):
+        return _cached(self, device, lambda: self.w.detach().float().to(device).contiguous(), "_fce_w")
+
+    def emit(self, be, xs, out=None):
+        h, w = xs[0].h, xs[0].w
+        y = out if out is not None else be.alloc(xs[0].n, self.output_ch, h, w)
+        wp = self._w32(be.device).data_ptr()
+        n = len(xs)
+        for i, (x, m) in enumerate(zip(xs, self.realign_convs)):
+            assert (x.h, x.w) == (h, w), "BiFPN_Concat inputs must share the spatial size"
+            if isinstance(m, nn.Identity):
+                be.wadd(x, y, (wp, n, i), accumulate=int(i > 0))
+            else:
+                m.emit(be, x, out=y, epilogue=N.EPI_ACCUM if i else N.EPI_WSTORE, fusion=(wp, n, i))
+        return y
+
+    def forward(self, x):
+        return _run_eager(self, list(x))
+
+
+def _dense(mod: nn.Conv2d, device):
+    """fp32 [out][in] matrix + bias of a 1x1 nn.Conv2d (device)."""
+
+    def build():
+        w = mod.weight.detach().float().reshape(mod.out_channels, -1).contiguous().to(device)
+        b = (mod.bias.detach().float() if mod.bias is not None else torch.zeros(mod.out_channels)).to(device)
+        return w, b.contiguous()
+
+    return _cached(mod, device, build, "_fce_dense")
+
+
+def _coord_desc(inp, oup, mid, heads, scale, mats, identity, device):
+    d = N.CoordDesc()
+    d.inp, d.oup, d.mid, d.heads, d.scale = inp, oup, mid, heads, float(scale)
+    for i, (w, b) in enumerate(mats):
+        d.w[i] = w.data_ptr()
+        d.b[i] = b.data_ptr()
+    if isinstance(identity, nn.Conv2d):
+        nat = conv_native(identity, None, False, device)
+        d.id_w, d.id_b = nat.w.data_ptr(), nat.b.data_ptr()
+    return d
+
+
+class CoordAtt(nn.Module):
+    """fce_block.py:65-116."""
+
+    def __init__(self, inp, oup, reduction=32):
+        super().__init__()
+        self.pool_h = nn.AdaptiveAvgPool2d((None, 1))
+        self.pool_w = nn.AdaptiveAvgPool2d((1, None))
+        mip = max(8, inp // reduction)
+        self.cv1 = Conv(inp, mip, k=1, s=1, p=0)
+        self.cv_h = nn.Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
+        self.cv_w = nn.Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
+        self.identity = nn.Conv2d(inp, oup, 1) if inp != oup else nn.Identity()
+
+    def emit(self, be, x, out=None):
+        inp, mip, oup = self.cv1.conv.in_channels, self.cv1.conv.out_channels, self.cv_h.out_channels
+
+        def build():
+            w, b = fold_bn(self.cv1.conv, getattr(self.cv1, "bn", None))
+            return w.reshape(mip, inp).contiguous().to(be.device), b.contiguous().to(be.device)
+
+        cv1 = _cached(self.cv1, be.device, build, "_fce_cv1")
+        d = _coord_desc(inp, oup, mip, 1, 1.0, [cv1, _dense(self.cv_h, be.device), _dense(self.cv_w, be.device)],
+                        self.identity, be.device)
+        y = out if out is not None else be.alloc(x.n, oup, x.h, x.w)
+        be.coord(1, d, x, y)
+        return y
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class CoordCrossAtt(nn.Module):
+    """fce_block.py:119-180 (oup must equal inp, Q3)."""
+
+    def __init__(self, inp, oup, reduction=32, num_heads=1):
+        super().__init__()
+        self.mip = max(8, inp // reduction)
+        self.num_heads = num_heads
+        self.scale = (self.mip // num_heads) ** -0.5
+        self.pool_h = nn.AdaptiveAvgPool2d((None, 1))
+        self.pool_w = nn.AdaptiveAvgPool2d((1, None))
+        self.cv1 = nn.Conv2d(inp, self.mip, kernel_size=1)
+        self.q_conv = nn.Conv2d(self.mip, self.mip, 1)
+        self.k_conv = nn.Conv2d(self.mip, self.mip, 1)
+        self.v_conv = nn.Conv2d(self.mip, self.mip, 1)
+        self.proj = nn.Conv2d(self.mip, oup, 1)
+        self.gate = nn.Sigmoid()
+
+    def emit(self, be, x, out=None):
+        inp, oup = self.cv1.in_channels, self.proj.out_channels
+        if inp != oup:
+            raise RuntimeError("CoordCrossAtt: oup != inp cannot broadcast x * y_att (reference fce_block.py:180)")
+        mats = [_dense(m, be.device) for m in (self.cv1, self.q_conv, self.k_conv, self.v_conv, self.proj)]
+        d = _coord_desc(inp, oup, self.mip, self.num_heads, self.scale, mats, None, be.device)
+        y = out if out is not None else be.alloc(x.n, oup, x.h, x.w)
+        be.coord(2, d, x, y)
+        return y
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+class BiCoordCrossAtt(nn.Module):
+    """fce_block.py:183-284: x * sigmoid(gate_h[H] + gate_w[W]) with axial cross-attention gates."""
+
+    def __init__(self, inp, oup, reduction=32, num_heads=4):
+        super().__init__()
+        self.num_heads = num_heads
+        self.dim_head = max(8, inp // reduction) // num_heads
+        self.mid_dim = self.dim_head * num_heads
+        self.scale = self.dim_head**-0.5
+        self.pool_h = nn.AdaptiveAvgPool2d((None, 1))
+        self.pool_w = nn.AdaptiveAvgPool2d((1, None))
+        self.proj_q_h = nn.Conv2d(inp, self.mid_dim, 1)
+        self.proj_k_h = nn.Conv2d(inp, self.mid_dim, 1)
+        self.proj_v_h = nn.Conv2d(inp, self.mid_dim, 1)
+        self.out_h = nn.Conv2d(self.mid_dim, oup, 1)
+        self.proj_q_w = nn.Conv2d(inp, self.mid_dim, 1)
+        self.proj_k_w = nn.Conv2d(inp, self.mid_dim, 1)
+        self.proj_v_w = nn.Conv2d(inp, self.mid_dim, 1)
+        self.out_w = nn.Conv2d(self.mid_dim, oup, 1)
+        self.gate = nn.Sigmoid()
+        self.identity = nn.Conv2d(inp, oup, 1) if inp != oup else nn.Identity()
+
+    def emit(self, be, x, out=None):
+        inp, oup = self.proj_q_h.in_channels, self.out_h.out_channels
+        mods = (self.proj_q_h, self.proj_k_h, self.proj_v_h, self.proj_q_w, self.proj_k_w, self.proj_v_w,
+                self.out_h, self.out_w)
+        d = _coord_desc(inp, oup, self.mid_dim, self.num_heads, self.scale, [_dense(m, be.device) for m in mods],
+                        self.identity, be.device)
+        y = out if out is not None else be.alloc(x.n, oup, x.h, x.w)
+        be.coord(0, d, x, y)
+        return y
+
+    def forward(self, x):
+        return _run_eager(self, x)
+
+
+# ============================================================================ head.py
+class DFL(nn.Module):
+    """block.py:58-80 (the fixed arange(c1) projection; the decode kernel applies it)."""
+
+    def __init__(self, c1=16):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, 1, 1, bias=False).requires_grad_(False)
+        x = torch.arange(c1, dtype=torch.float)
+        self.conv.weight.data[:] = nn.Parameter(x.view(1, c1, 1, 1))
+        self.c1 = c1
+
+
+class Detect(nn.Module):
+    """head.py:26-167 (legacy=False cls branch, Q5).  Inference returns (y, maps)."""
+
+    dynamic = False
+    export = False
+    end2end = False
+    max_det = 300
+    shape = None
+    legacy = False
+    xyxy = False
+
+    def __init__(self, nc=80, ch=()):
+        super().__init__()
+        self.nc = nc
+        self.nl = len(ch)
+        self.reg_max = 16
+        self.no = nc + self.reg_max * 4
+        self.stride = torch.zeros(self.nl)
+        c2, c3 = max((16, ch[0] // 4, self.reg_max * 4)), max(ch[0], min(self.nc, 100))
+        self.cv2 = nn.ModuleList(
+            nn.Sequential(Conv(x, c2, 3), Conv(c2, c2, 3), nn.Conv2d(c2, 4 * self.reg_max, 1)) for x in ch
+        )
+        self.cv3 = (
+            nn.ModuleList(nn.Sequential(Conv(x, c3, 3), Conv(c3, c3, 3), nn.Conv2d(c3, self.nc, 1)) for x in ch)
+            if self.legacy
+            else nn.ModuleList(
+                nn.Sequential(
+                    nn.Sequential(DWConv(x, x, 3), Conv(x, c3, 1)),
+                    nn.Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)),
+                    nn.Conv2d(c3, self.nc, 1),
+                )
+                for x in ch
+            )
+        )
+        self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
+
+    def strides(self):
+        s = [float(v) for v in self.stride]
+        if not all(s):
+            raise RuntimeError("Detect.stride is not set (DetectionModel sets [8, 16, 32])")
+        return s
+
+    def emit_maps(self, be, xs):
+        maps = []
+        for i, x in enumerate(xs):
+            mp = be.alloc(x.n, self.no, x.h, x.w, N.F32)  # cat(box, cls) (head.py:122), fp32 logits (Q11)
+            b = self.cv2[i][1].emit(be, self.cv2[i][0].emit(be, x))
+            emit_conv(be, self.cv2[i][2], None, False, b, out=mp.slice(0, 4 * self.reg_max))
+            seq = self.cv3[i]
+            if self.legacy:
+                c = seq[1].emit(be, seq[0].emit(be, x))
+            else:
+                c = seq[0][1].emit(be, seq[0][0].emit(be, x))
+                c = seq[1][1].emit(be, seq[1][0].emit(be, c))
+            emit_conv(be, seq[2], None, False, c, out=mp.slice(4 * self.reg_max, self.nc))
+            maps.append(mp)
+        return maps
+
+    def emit(self, be, xs, out=None):
+        maps = self.emit_maps(be, xs)
+        pred = be.detect(maps, self.strides(), self.reg_max)
+        return pred, maps
+
+    def forward(self, x):
+        xs = list(x)
+        dev = xs[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("Detect: fce_yolo_amd runs on ROCm devices only; no CPU fallback")
+        be = EagerBackend(dev)
+        views = [be.from_torch(t) for t in xs]
+        pred, maps = self.emit(be, views)
+        return pred, [be.to_torch(m, torch.float32) for m in maps]

@@ -1,0 +1,191 @@
+/*
+ * fce_yolo.h — C-ABI of the MI355X-native FCE-YOLOv11 inference path (libfceyolo.so).
+ *
+ * Plain C: pointers, sizes and POD descriptors only; no torch or C++ types.  Every
+ * function returns an int status (FCE_OK = 0); on failure fce_last_error() returns a
+ * thread-local message.  No C++ exception crosses this ABI.  Device pointers are HIP
+ * device allocations owned by the caller unless stated otherwise; `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream).  Nothing here synchronises or
+ * allocates inside a launch function, so every op may be captured into a hipGraph.
+ *
+ * Which reference interface each entry point replaces (ShioMisaka/fce-yolo, ultralytics/):
+ *   fce_conv2d            nn/modules/conv.py:39-89 Conv.forward_fuse (+BN fold torch_utils.py:237-267),
+ *                         conv.py:185-200 DWConv, head.py:86-107 the Detect 1x1 nn.Conv2d,
+ *                         block.py:474-476 Bottleneck residual, conv.py:616-641 Concat (channel-offset
+ *                         writes), block.py:303-307 C2f chunk (channel-offset reads), nn.Upsample (up=1 reads)
+ *   fce_maxpool_chain     block.py:228-232 SPPF's three chained MaxPool2d(5,1,2)
+ *   fce_weighted_add      nn/modules/fce_block.py:40-63 BiFPN_Concat weighted fusion (Identity branches)
+ *   fce_bicoordcrossatt   nn/modules/fce_block.py:183-284 BiCoordCrossAtt.forward
+ *   fce_coordatt          nn/modules/fce_block.py:65-116  CoordAtt.forward
+ *   fce_coordcrossatt     nn/modules/fce_block.py:119-180 CoordCrossAtt.forward
+ *   fce_psa_attention     nn/modules/block.py:1284-1304   Attention.forward (softmax(q^T k) v + pe(v))
+ *   fce_detect_decode     nn/modules/head.py:149-167 Detect._inference, block.py:76-79 DFL,
+ *                         utils/tal.py:352-376 make_anchors / dist2bbox
+ *   fce_nms               utils/nms.py:13-166 non_max_suppression + :239-296 TorchNMS.nms
+ *   fce_copy              the NCHW <-> NHWC / fp32 <-> fp16 edges a drop-in module needs
+ *   fce_net_*             nn/tasks.py:160-188 BaseModel._predict_once (graph executor) and
+ *                         nn/autobackend.py:667-700 / :912-926 (forward, warmup) in hipGraph form
+ */
+#ifndef FCE_YOLO_H
+#define FCE_YOLO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCE_ABI_VERSION 1
+
+/* status codes */
+#define FCE_OK 0
+#define FCE_ERR_INVALID 1     /* bad argument / shape */
+#define FCE_ERR_HIP 2         /* HIP runtime error */
+#define FCE_ERR_UNSUPPORTED 3 /* valid but not implemented configuration */
+
+/* dtypes / layouts / activations / epilogues */
+#define FCE_F16 0
+#define FCE_F32 1
+#define FCE_U8 2
+#define FCE_NHWC 0
+#define FCE_NCHW 1
+#define FCE_ACT_NONE 0
+#define FCE_ACT_SILU 1
+#define FCE_EPI_STORE 0  /* y = act(conv + b) [+ residual]                      */
+#define FCE_EPI_WSTORE 1 /* y = alpha * act(conv + b)          (first BiFPN term)  */
+#define FCE_EPI_ACCUM 2  /* y = y + alpha * act(conv + b)      (later BiFPN terms) */
+
+/* A 4-D activation view.  NHWC views may be a channel slice [coff, coff+c) of a buffer
+ * holding `cstride` channels per pixel (this is how Concat / chunk / split are free).
+ * NCHW views are dense (cstride = c, coff = 0). */
+typedef struct fce_tensor {
+  void* data;
+  int dtype;  /* FCE_F16 | FCE_F32 | FCE_U8 */
+  int layout; /* FCE_NHWC | FCE_NCHW */
+  int n, c, h, w;
+  int cstride;
+  int coff;
+} fce_tensor;
+
+const char* fce_last_error(void);
+int fce_abi_version(void);
+/* number of visible HIP devices (0 without a GPU); never fails */
+int fce_device_count(void);
+
+/* ---------------------------------------------------------------- convolution */
+typedef struct fce_conv_desc {
+  int cin, cout, k, stride; /* square kernel, pad = k/2 (conv.py:30-36 autopad) */
+  int groups;               /* 1 = dense, cin (== cout) = depthwise               */
+  int act;                  /* FCE_ACT_*                                          */
+  int up;                   /* input read through nearest x(1<<up) upsampling     */
+  int epilogue;             /* FCE_EPI_*                                          */
+  const float* fusion_w;    /* BiFPN raw weights (device, fp32): alpha =          */
+  int fusion_n, fusion_i;   /*   relu(w[i]) / (sum_j relu(w[j]) + 1e-4)           */
+} fce_conv_desc;
+
+/* Bytes of the packed fp16 weight image the conv kernels read (dense: MFMA fragment order;
+ * depthwise / stem: tap-major fp32). */
+size_t fce_conv_weight_bytes(const fce_conv_desc* d);
+/* Host-side packing of an OIHW fp32 weight (BN already folded) into that image. */
+int fce_conv_pack_weights(const fce_conv_desc* d, const float* w_oihw, void* packed_host);
+/* y = conv(x) with the desc's epilogue.  x: NHWC f16 (or NCHW f16/f32/u8 when cin <= 4:
+ * the stem path), y: NHWC f16 or f32, residual: NHWC f16 or NULL.  bias: cout fp32. */
+int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
+               const fce_tensor* residual, const fce_tensor* y, void* stream);
+
+/* ---------------------------------------------------------------- pooling / fusion */
+/* SPPF chain: y1 = maxpool_k(x), y2 = maxpool_k(y1), y3 = maxpool_k(y2), stride 1, -inf pad. */
+int fce_maxpool_chain(const fce_tensor* x, const fce_tensor* y1, const fce_tensor* y2, const fce_tensor* y3, int k,
+                      void* stream);
+/* BiFPN identity branch: y = (accumulate ? y : 0) + alpha_i * up(x). */
+int fce_weighted_add(const fce_tensor* x, int up, const float* fusion_w, int fusion_n, int fusion_i, int accumulate,
+                     const fce_tensor* y, void* stream);
+
+/* ---------------------------------------------------------------- FCE coordinate attention */
+typedef struct fce_coord_desc {
+  int inp, oup, mid, heads; /* mid = dim_head*heads (BiCoord) / mip (CoordAtt, CoordCrossAtt) */
+  float scale;              /* softmax scale                                                  */
+  /* fp32 device weights, row-major [out][in]; biases [out].  Usage per op:
+   *   BiCoordCrossAtt: w[0..5] = proj_q_h, proj_k_h, proj_v_h, proj_q_w, proj_k_w, proj_v_w (mid x inp),
+   *                    w[6] = out_h, w[7] = out_w (oup x mid)
+   *   CoordAtt:        w[0] = cv1 (mid x inp, BN folded, SiLU), w[1] = cv_h, w[2] = cv_w (oup x mid)
+   *   CoordCrossAtt:   w[0] = cv1 (mid x inp), w[1..3] = q_conv, k_conv, v_conv (mid x mid), w[4] = proj */
+  const float* w[8];
+  const float* b[8];
+  /* identity 1x1 conv when inp != oup (packed with fce_conv_pack_weights), else NULL */
+  const void* id_w;
+  const float* id_b;
+} fce_coord_desc;
+
+size_t fce_coord_workspace_bytes(const fce_coord_desc* d, int n, int h, int w);
+int fce_bicoordcrossatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t ws_bytes,
+                        void* stream);
+int fce_coordatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t ws_bytes,
+                 void* stream);
+int fce_coordcrossatt(const fce_coord_desc* d, const fce_tensor* x, const fce_tensor* y, void* ws, size_t ws_bytes,
+                      void* stream);
+
+/* ---------------------------------------------------------------- C2PSA attention */
+/* qkv: NHWC f16 with heads*(2*key_dim+head_dim) channels ([q|k|v] per head, block.py:1296);
+ * y: NHWC f16 with heads*head_dim channels = softmax(q^T k * key_dim^-0.5) v + pe(v);
+ * pe_w: (heads*head_dim) x 9 fp32 depthwise taps (BN folded), pe_b: fp32. */
+int fce_psa_attention(const fce_tensor* qkv, int heads, int key_dim, int head_dim, const float* pe_w,
+                      const float* pe_b, const fce_tensor* y, void* stream);
+
+/* ---------------------------------------------------------------- Detect */
+/* box[i]: NHWC f32 (4*reg_max ch), cls[i]: NHWC f32 (nc ch) for level i; out: (N, 4+nc, A) fp32,
+ * A = sum_i h_i*w_i; rows 0-3 = xywh * stride (DFL expectation, fp32), rows 4.. = sigmoid(cls). */
+int fce_detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
+                      float* out, void* stream);
+
+/* ---------------------------------------------------------------- NMS */
+size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
+/* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
+ * anchor indices, counts: N.  Bit-exact with the reference for distinct scores; ties in the
+ * score sort are broken by ascending anchor index. */
+int fce_nms(const float* pred, int n, int nc, int anchors, float conf_thres, float iou_thres, int max_det,
+            int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
+            void* stream);
+
+/* ---------------------------------------------------------------- layout / dtype edges */
+/* dst = src with layout / dtype conversion (same n,c,h,w). */
+int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream);
+
+/* ---------------------------------------------------------------- whole-graph executor */
+typedef struct fce_net fce_net;
+fce_net* fce_net_create(void);
+void fce_net_destroy(fce_net* net);
+/* Activation buffer: `c` channels at (H >> shift, W >> shift); dtype FCE_F16 or FCE_F32. */
+int fce_net_add_buffer(fce_net* net, int c, int shift, int dtype);
+/* ops reference buffers by id; channel slices by (coff, c).  -1 = the network input. */
+int fce_net_add_conv(fce_net* net, const fce_conv_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
+                     int res_buf, int res_coff, const void* w_packed, const float* bias);
+int fce_net_add_maxpool_chain(fce_net* net, int buf, int in_coff, int c, int k);
+int fce_net_add_weighted_add(fce_net* net, int in_buf, int in_coff, int c, int up, const float* fusion_w,
+                             int fusion_n, int fusion_i, int accumulate, int out_buf, int out_coff);
+int fce_net_add_coord(fce_net* net, int kind /*0 BiCoord,1 CoordAtt,2 CoordCross*/, const fce_coord_desc* d,
+                      int in_buf, int in_coff, int out_buf, int out_coff);
+int fce_net_add_psa_attention(fce_net* net, int qkv_buf, int heads, int key_dim, int head_dim, const float* pe_w,
+                              const float* pe_b, int out_buf, int out_coff);
+/* map_bufs[i]: f32 buffer of level i holding cat(box 4*reg_max, cls nc) channels (head.py:122) */
+int fce_net_add_detect(fce_net* net, int nl, const int* map_bufs, const float* strides, int reg_max);
+/* allocate the arena for (batch, H, W); invalidates any captured graph */
+int fce_net_plan(fce_net* net, int batch, int h, int w);
+size_t fce_net_arena_bytes(const fce_net* net);
+int fce_net_num_anchors(const fce_net* net);
+/* input: NCHW f16/f32/u8 (u8 is divided by 255 in the stem); pred: (batch, 4+nc, A) fp32.
+ * graph=1 captures the whole forward into a hipGraph on first use for these pointers and
+ * replays it afterwards (re-captured if the pointers change). */
+int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int graph, void* stream);
+/* Eager run recording a hipEvent pair around every op: ms[i] per op (cap entries). */
+int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int cap, void* stream);
+int fce_net_num_ops(const fce_net* net);
+/* name (kernel family), algorithmic bytes and flops of op i at the planned size */
+int fce_net_op_info(const fce_net* net, int i, char* name, int name_cap, double* bytes, double* flops);
+int fce_net_buffer(const fce_net* net, int id, fce_tensor* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FCE_YOLO_H */

@@ -1,0 +1,130 @@
+"""Shared test-case table: per-op golden fixtures -> (drop-in module, oracle function)."""
+
+from __future__ import annotations
+
+import torch
+
+import fce_pkg
+
+fce_pkg.load()
+from fce_yolo_amd import modules as M  # noqa: E402
+from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
+from oracle import fce_oracle as O  # noqa: E402
+
+# name: (module class, ctor args, oracle fn(sd, "m", x, args) or None, args for oracle)
+OPS = {
+    "bicoord_n": (M.BiCoordCrossAtt, (128, 128, 8, 4), O.bicoordcrossatt),
+    "bicoord_l_dh16": (M.BiCoordCrossAtt, (512, 512, 8, 4), O.bicoordcrossatt),
+    "bicoord_h8": (M.BiCoordCrossAtt, (512, 512, 8, 8), O.bicoordcrossatt),
+    "bicoord_oup": (M.BiCoordCrossAtt, (64, 96, 8, 2), O.bicoordcrossatt),
+    "bicoord_dh2": (M.BiCoordCrossAtt, (32, 32, 32, 4), O.bicoordcrossatt),
+    "bifpn_2": (M.BiFPN_Concat, ([64, 32], 32), O.bifpn_concat),
+    "bifpn_3": (M.BiFPN_Concat, ([16, 32, 32], 16), O.bifpn_concat),
+    "bifpn_id": (M.BiFPN_Concat, ([32, 32], 32), O.bifpn_concat),
+    "bifpn_negw": (M.BiFPN_Concat, ([24, 48, 24], 24), O.bifpn_concat),
+    "coordatt_same": (M.CoordAtt, (64, 64, 16), O.coordatt),
+    "coordatt_oup": (M.CoordAtt, (32, 48, 4), O.coordatt),
+    "coordcross": (M.CoordCrossAtt, (64, 64, 4, 2), O.coordcrossatt),
+    "coordcross_h1": (M.CoordCrossAtt, (32, 32, 8, 1), O.coordcrossatt),
+    "conv_k1": (M.Conv, (24, 40, 1, 1), lambda sd, p, x, a: O.conv(sd, p, x, 1)),
+    "conv_k3s1": (M.Conv, (16, 32, 3, 1), lambda sd, p, x, a: O.conv(sd, p, x, 1)),
+    "conv_k3s2": (M.Conv, (16, 24, 3, 2), lambda sd, p, x, a: O.conv(sd, p, x, 2)),
+    "conv_c3": (M.Conv, (3, 16, 3, 2), lambda sd, p, x, a: O.conv(sd, p, x, 2)),
+    "dwconv": (M.DWConv, (32, 32, 3), lambda sd, p, x, a: O.dwconv(sd, p, x)),
+    "sppf": (M.SPPF, (64, 64, 5), lambda sd, p, x, a: O.sppf(sd, p, x, 5)),
+    "c2psa": (M.C2PSA, (256, 256, 1), lambda sd, p, x, a: O.c2psa(sd, p, x, list(a))),
+    "c3k2_b": (M.C3k2, (32, 64, 1, False, 0.25), lambda sd, p, x, a: O.c3k2(sd, p, x, list(a))),
+    "c3k2_c3k": (M.C3k2, (64, 64, 2, True), lambda sd, p, x, a: O.c3k2(sd, p, x, list(a))),
+}
+
+
+def build_op(name, fx):
+    """Drop-in module with the fixture's weights (seeded, or stored for the modified case)."""
+    cls, args, _ = OPS[name]
+    mod = cls(*args)
+    sd = mod.state_dict()
+    if any(k.startswith("sd::") for k in fx):
+        new = {k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd::")}
+    else:
+        new = seeded_state_dict([(k, v.shape) for k, v in sd.items()], int(fx["seed"]))
+    mod.load_state_dict(new)
+    for m in mod.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eps = 1e-3
+    return mod.eval()
+
+
+def op_inputs(fx):
+    ins = [torch.from_numpy(fx[k]) for k in sorted(k for k in fx if k.startswith("in"))]
+    return ins
+
+
+def oracle_op(name, mod, inputs, dtype=torch.float64):
+    """Run the oracle restatement of op `name` on the module's weights."""
+    _, args, fn = OPS[name]
+    sd = {"m." + k: v for k, v in mod.state_dict().items()}
+    sd = O.cast_sd(O.fuse_state_dict(sd), dtype)
+    xs = [x.to(dtype) for x in inputs]
+    a = list(args)
+    if name.startswith("c2psa") or name.startswith("c3k2"):
+        a = list(args) if len(args) > 2 else [args[0], args[1], 1]
+    x = xs if len(xs) > 1 else xs[0]
+    with torch.no_grad():
+        return fn(sd, "m", x, a)
+
+
+def build_detect(fx):
+    det = M.Detect(80, (64, 128, 256))
+    det.stride = torch.tensor([8.0, 16.0, 32.0])
+    sd = det.state_dict()
+    det.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in sd.items()], int(fx["seed"])))
+    for m in det.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eps = 1e-3
+    return det.eval()
+
+
+def seeded_model(cfg_name, seed=0, mutate=None):
+    from fce_yolo_amd.parser import DetectionModel, load_cfg
+
+    d = load_cfg(cfg_name)
+    if mutate:
+        mutate(d)
+    model = DetectionModel(d)
+    sd = model.state_dict()
+    model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in sd.items()], seed))
+    return model.eval()
+
+
+def heads8(d):
+    for row in d["backbone"]:
+        if row[2] == "BiCoordCrossAtt":
+            row[3] = [512, 8, 8]
+
+
+E2E = {
+    # fixture key: (cfg, mutate)
+    "yolo11n-fce_160_b2": ("yolo11n-fce.yaml", None),
+    "yolo11n-fce_320_b1": ("yolo11n-fce.yaml", None),
+    "yolo11s-bifpn_160_b2": ("yolo11s-bifpn.yaml", None),
+    "yolo11m-fce-h8_128_b1": ("yolo11m-fce.yaml", heads8),
+    "yolo11l-fce_128_b1": ("yolo11l-fce.yaml", None),
+    "yolo11n_160_b1": ("yolo11n.yaml", None),
+}
+
+
+def e2e_input(key, fx):
+    s, b = key.split("_")[-2:]
+    s, b = int(s), int(b[1:])
+    x = torch.rand(b, 3, s, s, generator=torch.Generator().manual_seed(int(fx["x_seed"])))
+    return x
+
+
+def oracle_model(model, x, dtype=torch.float64):
+    from oracle.parse import parse
+
+    layers, save, _ = parse(model.yaml)
+    sd = O.cast_sd(O.fuse_state_dict(model.state_dict()), dtype)
+    with torch.no_grad():
+        return O.forward(layers, save, {"model." + k[len("model."):] if k.startswith("model.") else k: v
+                                        for k, v in sd.items()}, x.to(dtype))

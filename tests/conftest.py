@@ -1,0 +1,59 @@
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+sys.path.insert(0, str(ROOT))
+
+import fce_pkg  # noqa: E402
+
+fce_pkg.load()
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built libfceyolo.so")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def tables():
+    return json.loads((GOLDEN / "parser_tables.json").read_text())
+
+
+class _Npz:
+    def __init__(self, path):
+        self.z = np.load(path, allow_pickle=False)
+
+    def group(self, name):
+        pre = name + "/"
+        return {k[len(pre):]: self.z[k] for k in self.z.files if k.startswith(pre)}
+
+    def names(self):
+        return sorted({k.split("/")[0] for k in self.z.files})
+
+
+@pytest.fixture(scope="session")
+def ops_fx():
+    return _Npz(GOLDEN / "ops.npz")
+
+
+@pytest.fixture(scope="session")
+def e2e_fx():
+    return _Npz(GOLDEN / "e2e.npz")
+
+
+@pytest.fixture(scope="session")
+def nms_fx():
+    return _Npz(GOLDEN / "nms.npz")
+
+
+@pytest.fixture(scope="session")
+def device():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible ROCm device")
+    return torch.device("cuda:0")

@@ -1,0 +1,152 @@
+"""CPU: host-side logic of the product package — parser parity with the reference, state_dict
+layout of the drop-in modules, and the C-ABI library (loads, exports every declared symbol,
+host-only packing).  No GPU compute here."""
+
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+from fce_yolo_amd import _native as N
+from fce_yolo_amd import modules as M
+from fce_yolo_amd.parser import DetectionModel, load_cfg
+
+ROOT = Path(__file__).resolve().parents[1]
+CONFIGS = ["yolo11n-fce", "yolo11s-fce", "yolo11m-fce", "yolo11l-fce", "yolo11x-fce", "yolo11n-bifpn",
+           "yolo11s-bifpn", "yolo11m-bifpn", "yolo11n", "yolo11m", "yolo11m-fce-h8"]
+
+
+def _model(name):
+    if name.endswith("-h8"):
+        d = load_cfg(name[:-3] + ".yaml")
+        cases.heads8(d)
+        return DetectionModel(d)
+    return DetectionModel(name + ".yaml")
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_state_dict_matches_reference(name, tables):
+    """Same keys, same order, same shapes as the reference DetectionModel (drop-in checkpoint load)."""
+    m = _model(name)
+    ours = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert ours == tables[name]["state_dict"]
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_layer_table_matches_reference(name, tables):
+    m = _model(name)
+    rows = tables[name]["rows"]
+    assert len(rows) == len(m.model)
+    for layer, row in zip(m.model, rows):
+        assert layer.f == row["f"] and layer.np == row["np"]
+        assert type(layer).__name__ == row["type"]
+        assert str(layer.args).replace("'", "") == row["args"].replace("'", "")
+    assert m.save == tables[name]["save"]
+    assert type(m.model[-1]).legacy == tables[name]["legacy_detect"]
+    assert m.stride.tolist() == [8.0, 16.0, 32.0]
+
+
+def test_yolo11n_fce_param_count():
+    m = DetectionModel("yolo11n-fce.yaml")
+    assert sum(p.numel() for p in m.parameters()) == 2568281  # SURVEY §3B, measured on the reference
+
+
+def test_bifpn_double_width_quirk():
+    """Q1: BiFPN_Concat output = make_divisible(max(c1) * width, 8) -> 64/32/32/64 at n scale."""
+    m = DetectionModel("yolo11n-fce.yaml")
+    assert [m.model[i].output_ch for i in (14, 17, 20, 23)] == [64, 32, 32, 64]
+
+
+def test_coordcrossatt_oup_mismatch_raises():
+    mod = M.CoordCrossAtt(128, 256, 16, 2)
+
+    class Be:
+        device = torch.device("cpu")
+
+    with pytest.raises(RuntimeError, match="oup != inp"):
+        mod.emit(Be(), cases.__dict__.get("View", None) or type("V", (), {"n": 1, "h": 4, "w": 4})())
+
+
+def test_cpu_forward_fails_loudly():
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        M.Conv(8, 8, 3)(torch.zeros(1, 8, 4, 4))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        DetectionModel("yolo11n-fce.yaml")(torch.zeros(1, 3, 64, 64))
+
+
+def test_library_exports_every_declared_symbol():
+    header = (ROOT / "include" / "fce_yolo.h").read_text()
+    declared = set(re.findall(r"\b(fce_[a-z0-9_]+)\s*\(", header))
+    L = N.lib()
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert declared <= set(N.EXPORTED) | {"fce_net_create", "fce_net_destroy"}
+    assert L.fce_abi_version() == 1
+
+
+def test_device_count_without_gpu_is_safe():
+    n = N.lib().fce_device_count()
+    assert n >= 0
+
+
+def _pack_ref(w, cin, cout, k):
+    """Python statement of the dense MFMA fragment order (csrc/conv.hip conv_pack)."""
+    cpt, taps = cin // 8, k * k
+    nchunk = taps * cpt
+    nsteps = (nchunk + 3) // 4
+    cot = (cout + 15) // 16
+    out = np.zeros((cot, nsteps, 64, 8), np.float16)
+    for ct in range(cot):
+        for s in range(nsteps):
+            for l in range(64):
+                co, c = ct * 16 + (l & 15), s * 4 + (l >> 4)
+                if co < cout and c < nchunk:
+                    tap, ci = c // cpt, (c % cpt) * 8
+                    out[ct, s, l] = w[co, ci:ci + 8, tap // k, tap % k]
+    return out
+
+
+@pytest.mark.parametrize("cin,cout,k", [(8, 16, 3), (16, 8, 3), (32, 40, 1), (64, 80, 3), (24, 24, 1)])
+def test_dense_weight_packing(cin, cout, k):
+    w = np.random.default_rng(0).standard_normal((cout, cin, k, k)).astype(np.float32)
+    d = N.ConvDesc(cin, cout, k, 1, 1, 1, 0, 0, None, 0, 0)
+    nb = N.lib().fce_conv_weight_bytes(C.byref(d))
+    out = np.empty(nb, np.uint8)
+    N.call("fce_conv_pack_weights", C.byref(d), w.ctypes.data, out.ctypes.data)
+    assert np.array_equal(out.view(np.float16).reshape(-1), _pack_ref(w, cin, cout, k).reshape(-1))
+
+
+def test_dw_and_stem_packing():
+    w = np.random.default_rng(1).standard_normal((16, 1, 3, 3)).astype(np.float32)
+    d = N.ConvDesc(16, 16, 3, 1, 16, 1, 0, 0, None, 0, 0)
+    out = np.empty(N.lib().fce_conv_weight_bytes(C.byref(d)), np.uint8)
+    N.call("fce_conv_pack_weights", C.byref(d), w.ctypes.data, out.ctypes.data)
+    assert np.array_equal(out.view(np.float32).reshape(9, 16), w.reshape(16, 9).T)
+    w = np.random.default_rng(2).standard_normal((16, 3, 3, 3)).astype(np.float32)
+    d = N.ConvDesc(3, 16, 3, 2, 1, 1, 0, 0, None, 0, 0)
+    out = np.empty(N.lib().fce_conv_weight_bytes(C.byref(d)), np.uint8)
+    N.call("fce_conv_pack_weights", C.byref(d), w.ctypes.data, out.ctypes.data)
+    assert np.array_equal(out.view(np.float32).reshape(27, 16), w.reshape(16, 27).T)
+
+
+def test_error_path_reports_message():
+    d = N.ConvDesc(8, 8, 5, 1, 1, 1, 0, 0, None, 0, 0)
+    t = N.Tensor(None, N.F16, N.NHWC, 1, 8, 4, 4, 8, 0)
+    with pytest.raises(N.FceError, match="kernel size"):
+        N.call("fce_conv2d", C.byref(d), C.byref(t), 1, 1, None, C.byref(t), None)
+
+
+def test_fold_bn_matches_reference_fuse():
+    """modules.fold_bn == torch_utils.fuse_conv_and_bn restated in the oracle (eps 1e-3)."""
+    from oracle import fce_oracle as O
+
+    conv = M.Conv(16, 32, 3)
+    sd = {k: v for k, v in cases.seeded_model("yolo11n-fce.yaml").model[1].state_dict().items()}
+    conv.load_state_dict(sd)
+    w, b = M.fold_bn(conv.conv, conv.bn)
+    f = O.fuse_state_dict({"m." + k: v for k, v in conv.state_dict().items()})
+    assert torch.equal(w, f["m.conv.weight"]) and torch.allclose(b, f["m.conv.bias"], atol=1e-7)

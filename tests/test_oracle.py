@@ -1,0 +1,107 @@
+"""CPU: pin the oracle restatement to the reference's golden vectors (tests/golden, made by
+tests/golden/make_golden.py from the reference itself)."""
+
+import hashlib
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+from oracle import nms_oracle
+from oracle.parse import parse
+
+torch.set_num_threads(8)
+
+
+@pytest.mark.parametrize("name", list(cases.OPS))
+def test_oracle_ops_match_reference(name, ops_fx):
+    fx = ops_fx.group(name)
+    mod = cases.build_op(name, fx)
+    out = cases.oracle_op(name, mod, cases.op_inputs(fx), torch.float32)
+    ref = torch.from_numpy(fx["out"])
+    assert out.shape == ref.shape
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+def test_oracle_detect_matches_reference(ops_fx):
+    from oracle import fce_oracle as O
+
+    fx = ops_fx.group("detect")
+    det = cases.build_detect(fx)
+    sd = O.cast_sd(O.fuse_state_dict({"m." + k: v for k, v in det.state_dict().items()}), torch.float32)
+    feats = [torch.from_numpy(fx[f"in{i}"]) for i in range(3)]
+    maps = O.detect_head_maps(sd, "m", feats, 80)
+    for i in range(3):
+        assert torch.allclose(maps[i], torch.from_numpy(fx[f"map{i}"]), atol=1e-4, rtol=1e-4)
+    y = O.detect_decode(maps, [8.0, 16.0, 32.0], 80)
+    ref = torch.from_numpy(fx["out"])
+    assert (y - ref).abs().max().item() <= 1e-3
+
+
+@pytest.mark.parametrize("key", list(cases.E2E))
+def test_oracle_end_to_end_matches_reference(key, e2e_fx):
+    fx = e2e_fx.group(key)
+    cfg, mut = cases.E2E[key]
+    model = cases.seeded_model(cfg, 0, mut)
+    x = cases.e2e_input(key, fx)
+    assert hashlib.sha256(x.numpy().tobytes()).digest() == fx["x_sha256"].tobytes()
+    y = cases.oracle_model(model, x, torch.float32)
+    ref = torch.from_numpy(fx["y"])
+    box_err = (y[:, :4] - ref[:, :4]).abs().max().item() / ref[:, :4].abs().max().item()
+    cls_err = (y[:, 4:] - ref[:, 4:]).abs().max().item()
+    assert box_err < 1e-5 and cls_err < 1e-5, (box_err, cls_err)
+
+
+def test_oracle_640_digest(e2e_fx):
+    fx = e2e_fx.group("yolo11n-fce_640_b1")
+    model = cases.seeded_model("yolo11n-fce.yaml", 0)
+    x = torch.rand(1, 3, 640, 640, generator=torch.Generator().manual_seed(640))
+    y = cases.oracle_model(model, x, torch.float32).numpy()
+    ref_slice = fx["y_slice"]
+    assert np.abs(y[:, :, ::37] - ref_slice).max() <= 1e-3 * np.abs(ref_slice).max()
+    assert np.allclose(y.astype(np.float64).sum(2), fx["y_sum"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["designed_small", "designed_many", "none", "saturated_maxdet"])
+def test_oracle_nms_bit_exact(name, nms_fx):
+    fx = nms_fx.group(name)
+    dets, keeps = nms_oracle.non_max_suppression(fx["pred"])
+    for b in range(fx["pred"].shape[0]):
+        assert np.array_equal(keeps[b], fx[f"keep{b}"].reshape(-1).astype(np.int64)), b
+        assert np.array_equal(dets[b], fx[f"det{b}"].reshape(-1, 6)), b
+
+
+def test_oracle_nms_on_model_output(e2e_fx):
+    fx = e2e_fx.group("yolo11n-fce_160_b2")
+    dets, keeps = nms_oracle.non_max_suppression(fx["y"])
+    for b in range(2):
+        assert np.array_equal(keeps[b], fx[f"nms_keep{b}"].astype(np.int64))
+        assert np.array_equal(dets[b], fx[f"nms_det{b}"])
+
+
+def _cfg(name):
+    """The built-in graph data of the product package (restated from the reference YAMLs)."""
+    from fce_yolo_amd.parser import load_cfg
+
+    if name.endswith("-h8"):
+        d = load_cfg(name[:-3] + ".yaml")
+        cases.heads8(d)
+        return d
+    return load_cfg(name + ".yaml")
+
+
+@pytest.mark.parametrize("name", ["yolo11n-fce", "yolo11s-fce", "yolo11m-fce", "yolo11l-fce", "yolo11x-fce",
+                                  "yolo11n-bifpn", "yolo11s-bifpn", "yolo11m-bifpn", "yolo11n", "yolo11m",
+                                  "yolo11m-fce-h8"])
+def test_oracle_parser_layer_table(name, tables):
+    layers, save, legacy = parse(_cfg(name))
+    t = tables[name]
+    assert save == t["save"]
+    assert legacy == t["legacy_detect"]
+    for L, row in zip(layers, t["rows"]):
+        assert L["i"] == row["i"] and L["f"] == row["f"]
+        assert L["type"] == row["type"] or (L["type"] == "Upsample" and row["type"] == "Upsample")
+        assert str(L["args"]).replace("'", "") == row["args"].replace("'", ""), (L, row)
