@@ -53,6 +53,18 @@ class ConvDesc(C.Structure):
     ]
 
 
+class DetectEpi(C.Structure):
+    _fields_ = [
+        ("pred", C.c_void_p),
+        ("anchors", C.c_int),
+        ("anchor_offset", C.c_int),
+        ("nc", C.c_int),
+        ("reg_max", C.c_int),
+        ("part", C.c_int),
+        ("stride", C.c_float),
+    ]
+
+
 class CoordDesc(C.Structure):
     _fields_ = [
         ("inp", C.c_int),
@@ -81,6 +93,7 @@ _SIGS = {
     "fce_conv_weight_bytes": (_SZ, [_PCD]),
     "fce_conv_pack_weights": (_I, [_PCD, _P, _P]),
     "fce_conv2d": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _P]),
+    "fce_conv2d_detect": (_I, [_PCD, _PT, _P, _P, C.POINTER(DetectEpi), _P]),
     "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),
     "fce_weighted_add": (_I, [_PT, _I, _P, _I, _I, _I, _PT, _P]),
     "fce_coord_workspace_bytes": (_SZ, [_PCO, _I, _I, _I]),
@@ -101,6 +114,7 @@ _SIGS = {
     "fce_net_add_coord": (_I, [_P, _I, _PCO, _I, _I, _I, _I]),
     "fce_net_add_psa_attention": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I]),
     "fce_net_add_detect": (_I, [_P, _I, _P, _P, _I]),
+    "fce_net_add_conv_detect": (_I, [_P, _PCD, _I, _I, _I, _I, C.c_float, _I, _I, _P, _P]),
     "fce_net_plan": (_I, [_P, _I, _I, _I]),
     "fce_net_arena_bytes": (_SZ, [_P]),
     "fce_net_num_anchors": (_I, [_P]),

@@ -135,6 +135,12 @@ class EagerBackend:
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         N.call("fce_psa_attention", C.byref(self.t(qkv)), heads, kd, hd, pe_w, pe_b, C.byref(self.t(y)), self.stream)
 
+    def conv_detect(self, desc: N.ConvDesc, x: View, pred: torch.Tensor, anchors: int, offset: int, part: int,
+                    stride: float, nc: int, reg_max: int, w_ptr: int, b_ptr: int):
+        x = self.materialize(x)
+        e = N.DetectEpi(pred.data_ptr(), anchors, offset, nc, reg_max, part, float(stride))
+        N.call("fce_conv2d_detect", C.byref(desc), C.byref(self.t(x)), w_ptr, b_ptr, C.byref(e), self.stream)
+
     def detect(self, maps: list[View], strides: list[float], reg_max: int) -> torch.Tensor:
         nl = len(maps)
         A = sum(m.h * m.w for m in maps)
@@ -163,6 +169,8 @@ _ONE = _OneCache()
 
 class NetBackend:
     """Records ops into a native fce_net for an input of logical size (H, W)."""
+
+    fused_detect = True  # Detect tail fused into the last convs' epilogues (no fp32 maps)
 
     def __init__(self, H: int, W: int, device: torch.device):
         self.H, self.W = H, W
@@ -220,6 +228,12 @@ class NetBackend:
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         assert qkv.coff == 0 and qkv.c == qkv.cstride
         N.call("fce_net_add_psa_attention", self.net, qkv.buf, heads, kd, hd, pe_w, pe_b, y.buf, y.coff)
+
+    def conv_detect(self, desc: N.ConvDesc, x: View, part: int, level: int, stride: float, nc: int, reg_max: int,
+                    w_ptr: int, b_ptr: int):
+        assert x.up == 0
+        N.call("fce_net_add_conv_detect", self.net, C.byref(desc), x.buf, x.coff, part, level, float(stride), nc,
+               reg_max, w_ptr, b_ptr)
 
     def detect(self, maps: list[View], strides: list[float], reg_max: int):
         nl = len(maps)

@@ -19,6 +19,8 @@ size_t conv_weight_bytes(const fce_conv_desc& d);
 int conv_pack(const fce_conv_desc& d, const float* w, void* out);
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
            const fce_tensor& y, hipStream_t s);
+int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
+                  const fce_detect_epi& e, hipStream_t s);
 int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
                   hipStream_t s);
 int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor& y,
@@ -54,9 +56,9 @@ int check_nhwc(const fce_tensor* t, const char* name, int dtype) {
 
 using namespace fce;
 
-#define FCE_GUARD(body)                                    \
+#define FCE_GUARD(...)                                     \
   try {                                                    \
-    body                                                   \
+    __VA_ARGS__                                            \
   } catch (const std::exception& e) {                      \
     return fail(FCE_ERR_INVALID, std::string("exception: ") + e.what()); \
   } catch (...) {                                          \
@@ -85,6 +87,11 @@ int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w, const
                const fce_tensor* y, void* stream) {
   FCE_CHECK(d && x && w && bias && y, "fce_conv2d: null argument");
   FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream));)
+}
+int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
+                      const fce_detect_epi* e, void* stream) {
+  FCE_CHECK(d && x && w && bias && e, "fce_conv2d_detect: null argument");
+  FCE_GUARD(return conv2d_detect(*d, *x, w, bias, *e, S(stream));)
 }
 int fce_maxpool_chain(const fce_tensor* x, const fce_tensor* y1, const fce_tensor* y2, const fce_tensor* y3, int k,
                       void* stream) {
@@ -140,7 +147,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -167,6 +174,7 @@ struct OpDesc {
   int box[4] = {0, 0, 0, 0}, cls[4] = {0, 0, 0, 0};
   float strides[4] = {0, 0, 0, 0};
   int reg_max = 16;
+  int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT
 };
 
 }  // namespace
@@ -180,6 +188,7 @@ struct fce_net {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   int anchors = 0, nc = 0;
+  int level_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   const void* cap_in = nullptr;
@@ -266,6 +275,10 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
       fce_tensor y = net->view(op.out, op.out_coff, op.heads * op.head_dim);
       return psa_attention(x, op.heads, op.key_dim, op.head_dim, op.pe_w, op.pe_b, y, s);
     }
+    case OP_CONV_DETECT: {
+      fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, op.part, op.strides[0]};
+      return conv2d_detect(op.conv, x, op.w, op.b, e, s);
+    }
     case OP_DETECT: {
       fce_tensor bx[4], cl[4];
       for (int i = 0; i < op.nl; ++i) {
@@ -306,6 +319,14 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       if (op.res >= 0) *bytes += N * ohw * d.cout * 2;
       if (d.epilogue == FCE_EPI_ACCUM) *bytes += N * ohw * d.cout * 2;
       *flops = 2.0 * N * ohw * d.cout * d.k * d.k * (dw ? 1 : d.cin);
+      break;
+    }
+    case OP_CONV_DETECT: {
+      const fce_conv_desc& d = op.conv;
+      const double px = N * hw(op.in);
+      *name = op.part == 0 ? "conv1x1_detect_box" : "conv1x1_detect_cls";
+      *bytes = px * d.cin * 2 + px * (op.part == 0 ? 4 : d.cout) * 4 + double(conv_weight_bytes(d));
+      *flops = 2.0 * px * d.cout * d.cin;
       break;
     }
     case OP_MAXPOOL:
@@ -481,6 +502,30 @@ int fce_net_add_detect(fce_net* net, int nl, const int* maps, const float* strid
   return FCE_OK;
 }
 
+int fce_net_add_conv_detect(fce_net* net, const fce_conv_desc* d, int in, int in_coff, int part, int level,
+                            float stride, int nc, int reg_max, const void* w, const float* b) {
+  FCE_CHECK(net && d && w && b && valid_buf(net, in, false), "fce_net_add_conv_detect: bad argument");
+  FCE_CHECK(part == 0 || part == 1, "fce_net_add_conv_detect: part must be 0 (box) or 1 (cls)");
+  FCE_CHECK(level >= 0 && level < 8, "fce_net_add_conv_detect: level out of range");
+  OpDesc op;
+  op.kind = OP_CONV_DETECT;
+  op.conv = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->cin;
+  op.part = part;
+  op.level = level;
+  op.strides[0] = stride;
+  op.nc = nc;
+  op.reg_max = reg_max;
+  op.w = w;
+  op.b = b;
+  net->nc = nc;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
 int fce_net_plan(fce_net* net, int batch, int h, int w) {
   FCE_CHECK(net && batch > 0 && h > 0 && w > 0, "fce_net_plan: bad argument");
   FCE_CHECK(h % 32 == 0 && w % 32 == 0, "fce_net_plan: H and W must be multiples of 32 (max stride)");
@@ -503,6 +548,20 @@ int fce_net_plan(fce_net* net, int batch, int h, int w) {
         ws = std::max(ws, coord_ws_bytes(op.coord, batch, h >> net->bufs[op.in].shift, w >> net->bufs[op.in].shift));
       if (op.kind == OP_DETECT)
         for (int i = 0; i < op.nl; ++i) A += (h >> net->bufs[op.box[i]].shift) * (w >> net->bufs[op.box[i]].shift);
+    }
+    // fused Detect levels: anchor blocks in level order (head.py:155 torch.cat over levels)
+    int lv_hw[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nlv = 0;
+    for (const OpDesc& op : net->ops)
+      if (op.kind == OP_CONV_DETECT && op.part == 0) {
+        lv_hw[op.level] = (h >> net->bufs[op.in].shift) * (w >> net->bufs[op.in].shift);
+        nlv = std::max(nlv, op.level + 1);
+      }
+    if (nlv) {
+      A = 0;
+      for (int i = 0; i < nlv; ++i) {
+        net->level_off[i] = A;
+        A += lv_hw[i];
+      }
     }
     net->anchors = A;
     net->ws_bytes = ws;

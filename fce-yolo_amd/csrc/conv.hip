@@ -19,8 +19,11 @@
 namespace fce {
 
 // ============================================================================ packing (host)
+// nsteps K-steps of 32 (4 chunks of 8 input channels); each cout tile stores nalloc >= nsteps
+// fragments: rounded up to even (the main loop consumes steps in pairs) + 2 zero fragments, so the
+// branch-free prefetch of steps s+2 / s+3 never reads past the image.
 struct DenseGeom {
-  int cpt, taps, nchunk, nsteps, cotiles;
+  int cpt, taps, nchunk, nsteps, nalloc, cotiles;
 };
 static DenseGeom dense_geom(const fce_conv_desc& d) {
   DenseGeom g;
@@ -28,6 +31,7 @@ static DenseGeom dense_geom(const fce_conv_desc& d) {
   g.taps = d.k * d.k;
   g.nchunk = g.taps * g.cpt;
   g.nsteps = (g.nchunk + 3) / 4;
+  g.nalloc = ((g.nsteps + 1) & ~1) + 2;
   g.cotiles = (d.cout + 15) / 16;
   return g;
 }
@@ -39,7 +43,7 @@ size_t conv_weight_bytes(const fce_conv_desc& d) {
   if (is_stem(d)) return size_t(d.cin) * d.k * d.k * d.cout * sizeof(float);  // [cin*k*k][cout] fp32
   if (is_dw(d)) return size_t(d.k) * d.k * d.cin * sizeof(float);             // [k*k][c] fp32
   DenseGeom g = dense_geom(d);
-  return size_t(g.cotiles) * g.nsteps * 64 * 8 * sizeof(_Float16);
+  return size_t(g.cotiles) * g.nalloc * 64 * 8 * sizeof(_Float16);
 }
 
 int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
@@ -60,11 +64,11 @@ int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
   DenseGeom g = dense_geom(d);
   _Float16* o = static_cast<_Float16*>(out);
   for (int ct = 0; ct < g.cotiles; ++ct)
-    for (int s = 0; s < g.nsteps; ++s)
+    for (int s = 0; s < g.nalloc; ++s)
       for (int l = 0; l < 64; ++l) {
         const int co = ct * 16 + (l & 15);
         const int c = s * 4 + (l >> 4);
-        _Float16* dst = o + ((size_t(ct) * g.nsteps + s) * 64 + l) * 8;
+        _Float16* dst = o + ((size_t(ct) * g.nalloc + s) * 64 + l) * 8;
         for (int j = 0; j < 8; ++j) {
           float v = 0.f;
           if (co < d.cout && c < g.nchunk) {
@@ -78,6 +82,10 @@ int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
 }
 
 // ============================================================================ dense MFMA kernel
+// 16 zero bytes: the source of every out-of-image / padded-K B fragment (static device memory is
+// zero-initialised)
+__device__ __attribute__((aligned(16))) _Float16 g_zero_line[8];
+
 struct ConvArgs {
   const _Float16* x;  // input view base (already offset by coff)
   int N, Hs, Ws, xcs;  // source buffer spatial size, channel stride
@@ -94,13 +102,19 @@ struct ConvArgs {
   int act;
   const float* fw;
   int fn, fi;
-  int cpt, nchunk, nsteps;
+  int cpt, nchunk, nsteps;  // nsteps: even (loop runs in pairs)
+  int nalloc;               // fragments stored per cout tile (nsteps + 2 zero pad)
+  unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
   int vec_ok;
+  // fused Detect tail (OUT_DFL / OUT_CLS): pred (N, 4+nc, A) fp32
+  float* pred;
+  int det_A, det_a0, det_nc, det_hw, det_w;
+  float det_stride;
 };
 
-enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3 };
+enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3, OUT_DFL = 4, OUT_CLS = 5 };
 
-template <int KS, int RC, int RP, int OUT>
+template <int KS, int RC, int RP, int OUT, bool FAST>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -110,19 +124,31 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int cot0 = blockIdx.y * RC;
   const int cotiles = (a.cout + 15) >> 4;
 
-  // per-rep pixel decode for this lane's B column
-  int pn[RP], py[RP], px[RP];
-  bool pv[RP];
+  // Per pixel-rep (this lane's B column): element offset of the tap-(0,0) source pixel, and a
+  // bit mask of the taps that fall inside the image (zero padding = the other taps).  Computed
+  // once, so a B load in the K loop costs a bit test, a 64-bit add and a pointer select.
+  int64_t pbase[RP];
+  unsigned vmask[RP];
 #pragma unroll
   for (int p = 0; p < RP; ++p) {
     int pix = pix_base + p * 16 + col;
-    pv[p] = pix < a.P;
-    pix = pv[p] ? pix : 0;
+    const bool pv = pix < a.P;
+    pix = pv ? pix : 0;
     const int hw = a.Ho * a.Wo;
-    pn[p] = pix / hw;
-    const int r = pix - pn[p] * hw;
-    py[p] = (r / a.Wo) * a.stride - (KS / 2);
-    px[p] = (r % a.Wo) * a.stride - (KS / 2);
+    const int n = pix / hw;
+    const int r = pix - n * hw;
+    const int iy0 = (r / a.Wo) * a.stride - (KS / 2);
+    const int ix0 = (r % a.Wo) * a.stride - (KS / 2);
+    unsigned m = 0;
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) {
+      const int iy = iy0 + t / KS, ix = ix0 + t % KS;
+      m |= unsigned(pv && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win) << t;
+    }
+    vmask[p] = m;
+    // KS == 3 requires up == 0 (host materialises upsampled inputs first)
+    pbase[p] = KS == 1 ? nhwc_off(n, iy0 >> a.up, ix0 >> a.up, a.Hs, a.Ws, a.xcs)
+                       : (int64_t(n) * a.Hs + iy0) * a.Ws * int64_t(a.xcs) + int64_t(ix0) * a.xcs;
   }
 
   f4 acc[RC][RP];
@@ -131,69 +157,133 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // per-lane K-chunk cursor: chunk c = 4*s + grp  ->  (tap, cc)
-  int tap = 0, cc = grp;
-  while (cc >= a.cpt) {
-    cc -= a.cpt;
-    ++tap;
-  }
+  // Branch-free K loop: an out-of-image tap or padded K chunk loads a 16-byte zero line (address
+  // select, never a value mask), so no load is conditional and hipcc places counted vmcnt waits;
+  // two K-steps of fragments stay in flight (ring set 0 / set 1, unrolled: static indices).
+  // FAST (cin % 32 == 0): a K-step is 32 channels of ONE tap, so the (tap, step-in-tap) cursor is
+  // wave-uniform (scalar).  Otherwise each lane decodes its chunk c = 4s+grp with a magic divide.
   const h8* wfrag[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
     const int ct = min(cot0 + r, cotiles - 1);
-    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nsteps) * 64 + lane;
+    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
   }
-
-  auto load_b = [&](int tap_, int cc_, h8 (&b)[RP]) {
-    const int ky = KS == 1 ? 0 : tap_ / KS;
-    const int kx = KS == 1 ? 0 : tap_ - ky * KS;
-    const bool tap_ok = tap_ < KS * KS;
+  const h8* zline = reinterpret_cast<const h8*>(g_zero_line);
+  const int spt = a.cpt >> 2;  // K-steps per tap (FAST)
+  int lt = 0, ls = 0;          // load cursor: tap, step within tap (FAST)
+  auto tap_off = [&](int t) -> int64_t {
+    const int ky = (t * 11) >> 5;  // t / 3 for t < 9
+    return KS == 1 ? 0 : (int64_t(ky) * a.Ws + (t - ky * 3)) * a.xcs;
+  };
+  auto load_b = [&](int s, h8 (&b)[RP]) {
+    int t, ce;  // tap and element offset within the pixel's channels
+    if (FAST) {
+      t = lt;
+      ce = ls * 32 + grp * 8;
+      if (++ls == spt) {
+        ls = 0;
+        ++lt;
+      }
+    } else {
+      const unsigned c = unsigned(s * 4 + grp);
+      t = a.cpt == 1 ? int(c) : int(__umulhi(c, a.cmagic));
+      ce = (int(c) - t * a.cpt) * 8;
+    }
+    const int64_t toff = tap_off(t) + ce;
+    const bool tin = t < KS * KS;
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
-      const int iy = py[p] + ky, ix = px[p] + kx;
-      const bool ok = tap_ok && pv[p] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (ok) {
-        const int64_t off = nhwc_off(pn[p], iy >> a.up, ix >> a.up, a.Hs, a.Ws, a.xcs) + cc_ * 8;
-        v = *reinterpret_cast<const h8*>(a.x + off);
-      }
-      b[p] = v;
+      const bool ok = tin && ((vmask[p] >> (t & 31)) & 1u);
+      const h8* src = ok ? reinterpret_cast<const h8*>(a.x + pbase[p] + toff) : zline;
+      b[p] = *src;
     }
   };
-
-  h8 bcur[RP], bnext[RP];
-  h8 acur[RC], anext[RC];
-  load_b(tap, cc, bcur);
+  auto load_a = [&](int s, h8 (&w)[RC]) {
 #pragma unroll
-  for (int r = 0; r < RC; ++r) acur[r] = wfrag[r][0];
-
-  for (int s = 0; s < a.nsteps; ++s) {
-    // advance cursor and prefetch step s+1
-    cc += 4;
-    while (cc >= a.cpt) {
-      cc -= a.cpt;
-      ++tap;
-    }
-    const bool more = s + 1 < a.nsteps;
-    if (more) {
-      load_b(tap, cc, bnext);
-#pragma unroll
-      for (int r = 0; r < RC; ++r) anext[r] = wfrag[r][(s + 1) * 64];
-    }
+    for (int r = 0; r < RC; ++r) w[r] = wfrag[r][s * 64];
+  };
+  h8 b0[RP], b1[RP], a0[RC], a1[RC];
+  load_b(0, b0);
+  load_a(0, a0);
+  load_b(1, b1);
+  load_a(1, a1);
+  for (int s = 0; s < a.nsteps; s += 2) {  // nsteps rounded up to even: padded steps are zero
 #pragma unroll
     for (int r = 0; r < RC; ++r)
 #pragma unroll
-      for (int p = 0; p < RP; ++p)
-        acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(acur[r], bcur[p], acc[r][p], 0, 0, 0);
-    if (more) {
+      for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[r], b0[p], acc[r][p], 0, 0, 0);
+    load_b(s + 2, b0);
+    load_a(s + 2, a0);
 #pragma unroll
-      for (int p = 0; p < RP; ++p) bcur[p] = bnext[p];
+    for (int r = 0; r < RC; ++r)
 #pragma unroll
-      for (int r = 0; r < RC; ++r) acur[r] = anext[r];
-    }
+      for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[r], b1[p], acc[r][p], 0, 0, 0);
+    load_b(s + 3, b1);
+    load_a(s + 3, a1);
   }
 
   // ---------------------------------------------------------------- epilogue
+  if (OUT == OUT_DFL) {
+    // Detect box branch (head.py:161-162, block.py:76-79, tal.py:367-376): the 4 x 16 logits of a
+    // pixel live in tiles r = side, lanes {p, p+16, p+32, p+48} x 4 registers -> softmax expectation
+    // with two xor-shuffles, then xywh * stride into pred rows 0..3 (fp32 throughout).
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      float dist[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v[4], mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[r < RC ? r : 0][p][j] + a.bias[r * 16 + grp * 4 + j];
+          mx = fmaxf(mx, v[j]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float den = 0.f, num = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = expf(v[j] - mx);
+          den += e;
+          num = __fadd_rn(num, __fmul_rn(e, (float)(grp * 4 + j)));  // no FMA: match detect_decode
+        }
+        den += __shfl_xor(den, 16);
+        den += __shfl_xor(den, 32);
+        num += __shfl_xor(num, 16);
+        num += __shfl_xor(num, 32);
+        dist[r] = num / den;
+      }
+      const int pix = pix_base + p * 16 + col;
+      if (grp == 0 && pix < a.P) {
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        const float ax = (float)(q % a.det_w) + 0.5f, ay = (float)(q / a.det_w) + 0.5f;
+        const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
+        float* o = a.pred + int64_t(n) * (4 + a.det_nc) * a.det_A + a.det_a0 + q;
+        o[0] = (x1 + x2) / 2.0f * a.det_stride;
+        o[a.det_A] = (y1 + y2) / 2.0f * a.det_stride;
+        o[int64_t(2) * a.det_A] = (x2 - x1) * a.det_stride;
+        o[int64_t(3) * a.det_A] = (y2 - y1) * a.det_stride;
+      }
+    }
+    return;
+  }
+  if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int co0 = (cot0 + r) * 16 + grp * 4;
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        const int pix = pix_base + p * 16 + col;
+        if (pix >= a.P) continue;
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) o[int64_t(co0 + j) * a.det_A] = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+      }
+    }
+    return;
+  }
   float alpha = 1.f;
   if (OUT == OUT_WSTORE || OUT == OUT_ACCUM) alpha = fusion_alpha(a.fw, a.fn, a.fi);
 #pragma unroll
@@ -259,12 +349,15 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 }
 
 // ============================================================================ depthwise 3x3
+// HBM-bound (each input pixel read once from HBM, 9x from L2): grid = (row chunks, N*Ho), one
+// thread per (output pixel, 8 channels) with 32-bit index math; taps unrolled, weights [9][wcs].
 struct DwArgs {
   const _Float16* x;
   int N, H, W, xcs;
-  int C, stride, k;
+  int C, stride;
   int Ho, Wo;
-  const float* w;  // [k*k][C]
+  const float* w;  // [9][wcs] (wcs >= C: a channel slice of a wider packed table)
+  int wcs;
   const float* bias;
   _Float16* y;
   int ycs;
@@ -272,41 +365,64 @@ struct DwArgs {
 };
 
 __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
-  const int cg8 = a.C / 8;
-  const int64_t total = int64_t(a.N) * a.Ho * a.Wo * cg8;
-  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
-    const int g = int(t % cg8);
-    const int64_t pix = t / cg8;
-    const int ox = int(pix % a.Wo);
-    const int oy = int((pix / a.Wo) % a.Ho);
-    const int n = int(pix / (int64_t(a.Wo) * a.Ho));
-    const int c0 = g * 8;
-    float acc[8];
+  const int cg8 = a.C >> 3;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.Wo * cg8) return;
+  const int ox = idx / cg8, c0 = (idx - ox * cg8) * 8;
+  const int row = blockIdx.y, n = row / a.Ho, oy = row - n * a.Ho;
+  float acc[8];
+  {
+    const f4 b0 = *reinterpret_cast<const f4*>(a.bias + c0);
+    const f4 b1 = *reinterpret_cast<const f4*>(a.bias + c0 + 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = a.bias[c0 + j];
-    const int pad = a.k / 2;
-    for (int ky = 0; ky < a.k; ++ky) {
-      const int iy = oy * a.stride - pad + ky;
-      if (iy < 0 || iy >= a.H) continue;
-      for (int kx = 0; kx < a.k; ++kx) {
-        const int ix = ox * a.stride - pad + kx;
-        if (ix < 0 || ix >= a.W) continue;
-        const h8 v = *reinterpret_cast<const h8*>(a.x + nhwc_off(n, iy, ix, a.H, a.W, a.xcs) + c0);
-        const float* wt = a.w + (ky * a.k + kx) * a.C + c0;
-        const f4 w0 = *reinterpret_cast<const f4*>(wt);
-        const f4 w1 = *reinterpret_cast<const f4*>(wt + 4);
+    for (int j = 0; j < 4; ++j) {
+      acc[j] = b0[j];
+      acc[j + 4] = b1[j];
+    }
+  }
+  const _Float16* xn = a.x + int64_t(n) * a.H * a.W * a.xcs + c0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[j] += (float)v[j] * w0[j];
-          acc[j + 4] += (float)v[j + 4] * w1[j];
-        }
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * a.stride - 1 + ky;
+    if (iy < 0 || iy >= a.H) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * a.stride - 1 + kx;
+      if (ix < 0 || ix >= a.W) continue;
+      const h8 v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix) * a.xcs);
+      const float* wt = a.w + (ky * 3 + kx) * a.wcs + c0;
+      const f4 w0 = *reinterpret_cast<const f4*>(wt);
+      const f4 w1 = *reinterpret_cast<const f4*>(wt + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += (float)v[j] * w0[j];
+        acc[j + 4] += (float)v[j + 4] * w1[j];
       }
     }
-    h8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
-    *reinterpret_cast<h8*>(a.y + pix * a.ycs + c0) = o;
   }
+  h8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
+  *reinterpret_cast<h8*>(a.y + (int64_t(row) * a.Wo + ox) * a.ycs + c0) = o;
+}
+
+// depthwise 3x3 (pad 1) on NHWC f16 slices; w = [9][wcs] fp32 taps (BN folded), bias fp32 [C]
+int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
+              const fce_tensor& y, hipStream_t s) {
+  FCE_CHECK(x.c == y.c && x.c % 8 == 0 && wcs >= x.c && wcs % 4 == 0, "dwconv: channel mismatch");
+  FCE_CHECK(x.layout == FCE_NHWC && y.layout == FCE_NHWC && x.dtype == FCE_F16 && y.dtype == FCE_F16,
+            "dwconv: NHWC f16 views");
+  FCE_CHECK(x.cstride % 8 == 0 && x.coff % 8 == 0 && y.cstride % 8 == 0 && y.coff % 8 == 0,
+            "dwconv: slices must be 8-aligned");
+  const int Ho = (x.h - 1) / stride + 1, Wo = (x.w - 1) / stride + 1;
+  FCE_CHECK(y.n == x.n && y.h == Ho && y.w == Wo, "dwconv: output size mismatch");
+  if (int64_t(y.n) * Ho * Wo == 0) return FCE_OK;
+  FCE_CHECK(int64_t(y.n) * Ho < 65536 * 1024, "dwconv: too many output rows");
+  DwArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.n, x.h, x.w, x.cstride, x.c, stride, Ho, Wo,
+           w, wcs, bias, static_cast<_Float16*>(y.data) + y.coff, y.cstride, act};
+  dim3 grid((Wo * (x.c / 8) + 255) / 256, y.n * Ho);
+  hipLaunchKernelGGL(dwconv_kernel, grid, dim3(256), 0, s, a);
+  return launch_status("dwconv_kernel");
 }
 
 // ============================================================================ stem (NCHW input, cin <= 4)
@@ -392,38 +508,86 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 static int grid_cap(int64_t blocks) { return int(blocks < 65535 * 16 ? blocks : 65535 * 16); }
 
 template <int KS, int RC, int RP>
-static void launch_dense(const ConvArgs& a, int out_kind, dim3 grid, hipStream_t s) {
+static void launch_dense(const ConvArgs& a, int out_kind, bool fast, dim3 grid, hipStream_t s) {
+#define CONV_L(O, F) hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, O, F>), grid, dim3(256), 0, s, a)
+#define CONV_O(O)  \
+  if (fast)        \
+    CONV_L(O, true); \
+  else             \
+    CONV_L(O, false);
+  if (KS == 3) {  // 3x3 convs always store fp16 (Conv + BN + SiLU [+ residual])
+    CONV_O(OUT_F16);
+    return;
+  }
   switch (out_kind) {
     case OUT_F16:
-      hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, OUT_F16>), grid, dim3(256), 0, s, a);
+      CONV_O(OUT_F16);
       break;
     case OUT_F32:
-      hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, OUT_F32>), grid, dim3(256), 0, s, a);
+      CONV_O(OUT_F32);
       break;
     case OUT_WSTORE:
-      hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, OUT_WSTORE>), grid, dim3(256), 0, s, a);
+      CONV_O(OUT_WSTORE);
+      break;
+    case OUT_DFL:
+      CONV_O(OUT_DFL);
+      break;
+    case OUT_CLS:
+      CONV_O(OUT_CLS);
       break;
     default:
-      hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, OUT_ACCUM>), grid, dim3(256), 0, s, a);
+      CONV_O(OUT_ACCUM);
       break;
   }
+#undef CONV_O
+#undef CONV_L
 }
 
-template <int KS>
-static void launch_dense_rc(const ConvArgs& a, int out_kind, int rc, hipStream_t s) {
-  constexpr int RP = 2;
+template <int KS, int RP>
+static void launch_dense_rp(const ConvArgs& a, int out_kind, bool fast, int rc, hipStream_t s) {
   const int cotiles = (a.cout + 15) / 16;
   dim3 grid((a.P + 64 * RP - 1) / (64 * RP), (cotiles + rc - 1) / rc);
   if (rc == 1)
-    launch_dense<KS, 1, RP>(a, out_kind, grid, s);
+    launch_dense<KS, 1, RP>(a, out_kind, fast, grid, s);
   else if (rc == 2)
-    launch_dense<KS, 2, RP>(a, out_kind, grid, s);
+    launch_dense<KS, 2, RP>(a, out_kind, fast, grid, s);
   else
-    launch_dense<KS, 4, RP>(a, out_kind, grid, s);
+    launch_dense<KS, 4, RP>(a, out_kind, fast, grid, s);
 }
 
-int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s) {
+// Tile choice: a wave owns (16*RC couts) x (16*RP pixels).  Big tiles reuse each loaded fragment
+// more; small layers (20x20, 40x40 maps) need more waves in flight to hide load latency, so the
+// tile shrinks until the launch has >= ~4 waves per SIMD (4096 waves on 256 CUs) or hits 1x1.
+static void pick_tile(int P, int cotiles, bool need_rc4, int* rc, int* rp) {
+  constexpr int64_t kTargetWaves = 4096;
+  int c = cotiles >= 4 ? 4 : cotiles >= 2 ? 2 : 1;
+  int p = 4;
+  auto waves = [&](int c_, int p_) { return int64_t((P + 16 * p_ - 1) / (16 * p_)) * ((cotiles + c_ - 1) / c_); };
+  while (waves(c, p) < kTargetWaves) {
+    if (p > 1) {
+      p /= 2;
+    } else if (c > 1 && !need_rc4) {
+      c /= 2;
+    } else {
+      break;
+    }
+  }
+  *rc = c;
+  *rp = p;
+}
+
+template <int KS>
+static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, int rp, hipStream_t s) {
+  if (rp == 1)
+    launch_dense_rp<KS, 1>(a, out_kind, fast, rc, s);
+  else if (rp == 2)
+    launch_dense_rp<KS, 2>(a, out_kind, fast, rc, s);
+  else
+    launch_dense_rp<KS, 4>(a, out_kind, fast, rc, s);
+}
+
+int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
+                const fce_tensor& y, const fce_detect_epi* det, hipStream_t s) {
   FCE_CHECK(d.k == 1 || d.k == 3 || (is_stem(d) && d.k <= 7), "conv: kernel size must be 1 or 3");
   FCE_CHECK(d.stride >= 1 && d.stride <= 2, "conv: stride must be 1 or 2");
   FCE_CHECK(x.n == y.n && x.c == d.cin && y.c == d.cout, "conv: channel/batch mismatch");
@@ -473,19 +637,21 @@ int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const flo
 
   if (is_dw(d)) {
     FCE_CHECK(d.groups == d.cin && d.cin == d.cout && d.cin % 8 == 0, "dwconv: groups == cin == cout, cin % 8 == 0");
-    FCE_CHECK(y.dtype == FCE_F16 && d.up == 0 && res == nullptr && d.epilogue == FCE_EPI_STORE,
-              "dwconv: plain f16 store only");
-    FCE_CHECK(y.cstride % 8 == 0 && y.coff % 8 == 0, "dwconv: output slice must be 8-aligned");
-    DwArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.n, x.h, x.w, x.cstride, d.cin, d.stride, d.k, Ho, Wo,
-             static_cast<const float*>(w), bias, static_cast<_Float16*>(y.data) + y.coff, y.cstride, d.act};
-    const int64_t total = int64_t(x.n) * Ho * Wo * (d.cin / 8);
-    hipLaunchKernelGGL(dwconv_kernel, dim3(grid_cap((total + 255) / 256)), dim3(256), 0, s, a);
-    return launch_status("dwconv_kernel");
+    FCE_CHECK(y.dtype == FCE_F16 && d.up == 0 && res == nullptr && d.epilogue == FCE_EPI_STORE && d.k == 3,
+              "dwconv: 3x3, plain f16 store only");
+    return dwconv3x3(x, d.stride, static_cast<const float*>(w), d.cin, bias, d.act, y, s);
   }
 
   FCE_CHECK(d.cin % 8 == 0, "conv: cin must be a multiple of 8");
   int out_kind;
-  if (y.dtype == FCE_F32) {
+  if (det) {
+    FCE_CHECK(det->pred && det->part >= 0 && det->part <= 1 && d.k == 1 && d.up == 0 && res == nullptr,
+              "conv detect epilogue: 1x1 conv into pred");
+    FCE_CHECK(det->part == 1 || (d.cout == 4 * det->reg_max && det->reg_max == 16),
+              "conv detect epilogue: box branch needs 4 x reg_max(16) outputs");
+    FCE_CHECK(det->part == 0 || d.cout == det->nc, "conv detect epilogue: cls branch needs nc outputs");
+    out_kind = det->part == 0 ? OUT_DFL : OUT_CLS;
+  } else if (y.dtype == FCE_F32) {
     FCE_CHECK(d.epilogue == FCE_EPI_STORE && res == nullptr, "conv: f32 output supports plain store only");
     out_kind = OUT_F32;
   } else {
@@ -524,15 +690,41 @@ int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const flo
   a.fi = d.fusion_i;
   a.cpt = g.cpt;
   a.nchunk = g.nchunk;
-  a.nsteps = g.nsteps;
+  a.nsteps = (g.nsteps + 1) & ~1;
+  a.nalloc = g.nalloc;
+  a.cmagic = g.cpt > 1 ? unsigned(0xFFFFFFFFull / unsigned(g.cpt) + 1ull) : 0u;
+  FCE_CHECK(g.nalloc >= a.nsteps + 2 && g.nchunk + 16 < 65536, "conv: K too large for the chunk cursor");
   a.vec_ok = (y.cstride % 4 == 0 && y.coff % 4 == 0 && (!res || (res->cstride % 4 == 0 && res->coff % 4 == 0))) ? 1 : 0;
   if (out_kind == OUT_WSTORE || out_kind == OUT_ACCUM) FCE_CHECK(d.fusion_w && d.fusion_n > d.fusion_i, "conv: fusion weights");
-  const int rc = g.cotiles >= 4 ? 4 : g.cotiles >= 2 ? 2 : 1;
+  a.pred = det ? det->pred : nullptr;
+  a.det_A = det ? det->anchors : 0;
+  a.det_a0 = det ? det->anchor_offset : 0;
+  a.det_nc = det ? det->nc : 0;
+  a.det_hw = Ho * Wo;
+  a.det_w = Wo;
+  a.det_stride = det ? det->stride : 0.f;
+  int rc, rp;
+  pick_tile(a.P, g.cotiles, out_kind == OUT_DFL, &rc, &rp);
+  if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
+  if (d.k == 3) FCE_CHECK(d.up == 0 && out_kind == OUT_F16, "conv 3x3: plain fp16 store, no fused upsampling");
+  const bool fast = d.cin % 32 == 0;
   if (d.k == 1)
-    launch_dense_rc<1>(a, out_kind, rc, s);
+    launch_dense_rc<1>(a, out_kind, fast, rc, rp, s);
   else
-    launch_dense_rc<3>(a, out_kind, rc, s);
+    launch_dense_rc<3>(a, out_kind, fast, rc, rp, s);
   return launch_status("conv_mfma_kernel");
+}
+
+int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
+           const fce_tensor& y, hipStream_t s) {
+  return conv2d_impl(d, x, w, bias, res, y, nullptr, s);
+}
+
+int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
+                  const fce_detect_epi& e, hipStream_t s) {
+  // the output view only carries the spatial geometry; results go to e.pred
+  fce_tensor y{nullptr, FCE_F32, FCE_NHWC, x.n, d.cout, x.h, x.w, d.cout, 0};
+  return conv2d_impl(d, x, w, bias, nullptr, y, &e, s);
 }
 
 }  // namespace fce

@@ -1,13 +1,16 @@
 // FCE coordinate-attention operators (reference ultralytics/nn/modules/fce_block.py):
 //   BiCoordCrossAtt  :183-284   CoordAtt :65-116   CoordCrossAtt :119-180
 //
-// All three are HBM-bound passes over x (NHWC fp16) around a tiny per-image computation:
-//   1. pool:   xh[n][y][c] = mean_x x      (row kernel: one block per (n, y), LDS tree reduce)
-//              xw[n][x][c] = mean_y x      (column kernel: per (n, y-chunk, x-chunk) partial sums,
-//                                           reduced in fixed order by the compute kernel)
-//   2. compute (per image): 1x1 projections, axial softmax attention, output projection -> gates
-//      (fp32 throughout; deterministic, no atomics)
-//   3. apply:  y = id(x) * gate  (vectorised 16-byte NHWC pass; id = optional 1x1 conv into y first)
+// All three are HBM-bound passes over x (NHWC fp16) around a small per-image computation:
+//   1. pool:    xh[n][y][c] = mean_x x   (one block per (n, y): 16-byte loads, LDS tree reduce)
+//               xw[n][x][c] = mean_y x   (one block per (n, column strip): each thread owns 8 channels
+//                                         of one column and walks all rows; no cross-thread reduce)
+//   2. project: 1x1 convs on the pooled vectors as "jobs" (src rows staged in LDS, weights stored
+//               transposed [in][out] so a wave reads one contiguous row per input channel)
+//   3. attend:  axial softmax attention per (image, branch, query tile) with K/V in LDS, online
+//               softmax in registers, then the output projection from LDS -> gates (fp32)
+//   4. apply:   y = id(x) * gate, one vectorised 16-byte NHWC pass (id = optional 1x1 conv into y first)
+// Everything is deterministic (fixed reduction orders, no atomics).
 #include "common.h"
 
 namespace fce {
@@ -15,46 +18,39 @@ namespace fce {
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
            const fce_tensor& y, hipStream_t s);
 
-static constexpr int ROWS_PER_CHUNK = 16;
+enum { ACT_NONE_ = 0, ACT_SILU_ = 1, ACT_SIGMOID_ = 2 };
 
 struct CoordWs {
-  float* xh;       // N*H*C
-  float* colpart;  // N*YC*W*C
-  float* scratch;  // per op
-  float* g1;       // N*H*oup (gate_h / a_h / y_att)
-  float* g2;       // N*W*oup (gate_w / a_w)
-  int YC;
+  float* xh;      // N*H*C
+  float* xw;      // N*W*C
+  float* buf[6];  // N*L*mid each
+  float* g1;      // N*H*oup
+  float* g2;      // N*W*oup
 };
 
 static size_t align_f(size_t n) { return (n + 63) & ~size_t(63); }
 
-static size_t scratch_floats(int kind, const fce_coord_desc& d, int h, int w) {
+static size_t ws_layout(const fce_coord_desc& d, int n, int h, int w, CoordWs* out, float* base) {
   const int L = h > w ? h : w;
-  if (kind == 0) return size_t(2) * 4 * L * d.mid;  // per image: 2 branches x (q,k,v,y)
-  return size_t(h + w) * d.mid * 4;                 // per image: y (+ q,k,v,z for CoordCross)
-}
-
-static size_t ws_floats(int kind, const fce_coord_desc& d, int n, int h, int w, CoordWs* out, float* base) {
-  const int YC = (h + ROWS_PER_CHUNK - 1) / ROWS_PER_CHUNK;
+  const int mx = d.mid > d.oup ? d.mid : d.oup;
   size_t off = 0;
-  size_t xh = align_f(size_t(n) * h * d.inp), col = align_f(size_t(n) * YC * w * d.inp);
-  size_t sc = align_f(size_t(n) * scratch_floats(kind, d, h, w));
-  size_t g1 = align_f(size_t(n) * h * d.oup), g2 = align_f(size_t(n) * w * d.oup);
-  if (out) {
-    out->xh = base + off;
-    out->colpart = base + off + xh;
-    out->scratch = base + off + xh + col;
-    out->g1 = base + off + xh + col + sc;
-    out->g2 = base + off + xh + col + sc + g1;
-    out->YC = YC;
-  }
-  return xh + col + sc + g1 + g2;
+  auto take = [&](size_t cnt) {
+    float* p = base ? base + off : nullptr;
+    off += align_f(cnt);
+    return p;
+  };
+  CoordWs ws;
+  ws.xh = take(size_t(n) * h * d.inp);
+  ws.xw = take(size_t(n) * w * d.inp);
+  for (int i = 0; i < 6; ++i) ws.buf[i] = take(size_t(n) * L * mx);
+  ws.g1 = take(size_t(n) * h * d.oup);
+  ws.g2 = take(size_t(n) * w * d.oup);
+  if (out) *out = ws;
+  return off;
 }
 
 size_t coord_ws_bytes(const fce_coord_desc& d, int n, int h, int w) {
-  size_t m = 0;
-  for (int k = 0; k < 3; ++k) m = std::max(m, ws_floats(k, d, n, h, w, nullptr, nullptr));
-  return m * sizeof(float);
+  return ws_layout(d, n, h, w, nullptr, nullptr) * sizeof(float);
 }
 
 // ---------------------------------------------------------------------------- 1. pooling
@@ -85,9 +81,8 @@ __global__ __launch_bounds__(256) void pool_rows_kernel(const _Float16* x, int x
   }
 }
 
-__global__ __launch_bounds__(256) void pool_cols_kernel(const _Float16* x, int xcs, int H, int W, int C,
-                                                        float* colpart, int YC) {
-  const int n = blockIdx.z, yc = blockIdx.y;
+__global__ __launch_bounds__(256) void pool_cols_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xw) {
+  const int n = blockIdx.y;
   const int CG = C / 8;
   const int XW = 256 / CG;
   const int t = threadIdx.x;
@@ -95,178 +90,140 @@ __global__ __launch_bounds__(256) void pool_cols_kernel(const _Float16* x, int x
   const int xx = blockIdx.x * XW + xi;
   if (xi >= XW || xx >= W) return;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int y0 = yc * ROWS_PER_CHUNK, y1 = min(H, y0 + ROWS_PER_CHUNK);
-  for (int y = y0; y < y1; ++y) {
-    const h8 v = *reinterpret_cast<const h8*>(x + nhwc_off(n, y, xx, H, W, xcs) + cg * 8);
+  const _Float16* p = x + nhwc_off(n, 0, xx, H, W, xcs) + cg * 8;
+  const int64_t rs = int64_t(W) * xcs;
+  int y = 0;
+  for (; y + 1 < H; y += 2) {
+    const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
+    const h8 v1 = *reinterpret_cast<const h8*>(p + (y + 1) * rs);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v1[j];
   }
-  float* o = colpart + ((int64_t(n) * YC + yc) * W + xx) * C + cg * 8;
+  if (y < H) {
+    const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = acc[j];
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+  }
+  const float inv = 1.0f / (float)H;
+  float* o = xw + (int64_t(n) * W + xx) * C + cg * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = acc[j] * inv;
 }
 
-// xw[x][c] for image n, reduced in fixed chunk order
-__device__ __forceinline__ float xw_at(const float* colpart, int n, int YC, int W, int C, int xx, int c, float invH) {
-  float s = 0.f;
-  for (int k = 0; k < YC; ++k) s += colpart[((int64_t(n) * YC + k) * W + xx) * C + c];
-  return s * invH;
-}
-
-// ---------------------------------------------------------------------------- 2. compute
-struct CoordArgs {
-  fce_coord_desc d;
-  int H, W;
-  CoordWs ws;
+// ---------------------------------------------------------------------------- 2. projections
+struct ProjJob {
+  const float* src;  // [N][L][K]
+  const float* wt;   // [K][M]  (transposed 1x1 weight)
+  const float* b;    // [M]
+  float* dst;        // [N][L][M]
+  int L, K, M, act;
+};
+struct ProjArgs {
+  ProjJob job[6];
 };
 
-// out[i][m] = act(sum_c Wt[m][c] * src(i, c) + b[m]) for i < L, m < M; src given by a functor
-template <typename Src>
-__device__ void proj(const float* Wt, const float* b, int M, int K, int L, Src src, float* out, int act) {
-  for (int e = threadIdx.x; e < L * M; e += blockDim.x) {
-    const int i = e / M, m = e % M;
-    const float* wr = Wt + int64_t(m) * K;
-    float s = b ? b[m] : 0.f;
-    for (int c = 0; c < K; ++c) s += wr[c] * src(i, c);
-    out[int64_t(i) * M + m] = act == 1 ? silu(s) : s;
-  }
+__device__ __forceinline__ float act_f(float v, int act) {
+  return act == ACT_SILU_ ? v / (1.0f + expf(-v)) : act == ACT_SIGMOID_ ? 1.0f / (1.0f + expf(-v)) : v;
 }
 
-// y[i][h*dh+d] = sum_j softmax_j(scale * q_i . k_j) v[j][h*dh+d]  (per head, axial)
-__device__ void axial_attention(const float* q, const float* k, const float* v, int Lq, int Lk, int mid, int heads,
-                                float scale, float* y) {
-  const int dh = mid / heads;
-  for (int e = threadIdx.x; e < Lq * heads; e += blockDim.x) {
-    const int i = e / heads, hd = e % heads;
-    const float* qi = q + int64_t(i) * mid + hd * dh;
-    float mx = -INFINITY;
-    for (int j = 0; j < Lk; ++j) {
-      const float* kj = k + int64_t(j) * mid + hd * dh;
-      float s = 0.f;
-      for (int d = 0; d < dh; ++d) s += qi[d] * kj[d];
-      mx = fmaxf(mx, s * scale);
-    }
-    float den = 0.f;
-    for (int j = 0; j < Lk; ++j) {
-      const float* kj = k + int64_t(j) * mid + hd * dh;
-      float s = 0.f;
-      for (int d = 0; d < dh; ++d) s += qi[d] * kj[d];
-      den += expf(s * scale - mx);
-    }
-    const float inv = 1.0f / den;
-    for (int d0 = 0; d0 < dh; d0 += 16) {
-      float acc[16];
-#pragma unroll
-      for (int t = 0; t < 16; ++t) acc[t] = 0.f;
-      for (int j = 0; j < Lk; ++j) {
-        const float* kj = k + int64_t(j) * mid + hd * dh;
-        float s = 0.f;
-        for (int d = 0; d < dh; ++d) s += qi[d] * kj[d];
-        const float p = expf(s * scale - mx) * inv;
-        const float* vj = v + int64_t(j) * mid + hd * dh + d0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-          if (d0 + t < dh) acc[t] += p * vj[t];
-      }
-      for (int t = 0; t < 16 && d0 + t < dh; ++t) y[int64_t(i) * mid + hd * dh + d0 + t] = acc[t];
-    }
-  }
-}
-
-__device__ __forceinline__ void block_sync_global() {
-  __threadfence_block();
+// grid (position tiles, jobs, N); tile of TP positions staged in LDS
+__global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const ProjJob& jb = pa.job[blockIdx.y];
+  const int n = blockIdx.z;
+  const int p0 = blockIdx.x * TP;
+  if (p0 >= jb.L) return;
+  const int np = min(TP, jb.L - p0);
+  const float* src = jb.src + (int64_t(n) * jb.L + p0) * jb.K;
+  for (int e = threadIdx.x; e < np * jb.K; e += blockDim.x) sm[e] = src[e];
   __syncthreads();
-}
-
-// BiCoordCrossAtt: grid (N, 2): branch 0 = H branch (q from x_h, k/v from x_w) -> gate_h[H][oup]
-//                                branch 1 = W branch (q from x_w, k/v from x_h) -> gate_w[W][oup]
-__global__ __launch_bounds__(256) void bicoord_compute_kernel(CoordArgs a) {
-  const int n = blockIdx.x, br = blockIdx.y;
-  const int C = a.d.inp, H = a.H, W = a.W, mid = a.d.mid, YC = a.ws.YC;
-  const int L = H > W ? H : W;
-  float* base = a.ws.scratch + (int64_t(n) * 2 + br) * 4 * L * mid;
-  float *q = base, *k = base + L * mid, *v = base + 2 * L * mid, *y = base + 3 * L * mid;
-  const float* xh = a.ws.xh + int64_t(n) * H * C;
-  const float* colp = a.ws.colpart;
-  const float invH = 1.0f / (float)H;
-  auto src_h = [&](int i, int c) { return xh[int64_t(i) * C + c]; };
-  auto src_w = [&](int i, int c) { return xw_at(colp, n, YC, W, C, i, c, invH); };
-  const int Lq = br == 0 ? H : W, Lk = br == 0 ? W : H;
-  const int wq = br == 0 ? 0 : 3;  // weight index base: q,k,v
-  if (br == 0) {
-    proj(a.d.w[wq + 0], a.d.b[wq + 0], mid, C, Lq, src_h, q, 0);
-    proj(a.d.w[wq + 1], a.d.b[wq + 1], mid, C, Lk, src_w, k, 0);
-    proj(a.d.w[wq + 2], a.d.b[wq + 2], mid, C, Lk, src_w, v, 0);
-  } else {
-    proj(a.d.w[wq + 0], a.d.b[wq + 0], mid, C, Lq, src_w, q, 0);
-    proj(a.d.w[wq + 1], a.d.b[wq + 1], mid, C, Lk, src_h, k, 0);
-    proj(a.d.w[wq + 2], a.d.b[wq + 2], mid, C, Lk, src_h, v, 0);
+  float* dst = jb.dst + (int64_t(n) * jb.L + p0) * jb.M;
+  for (int e = threadIdx.x; e < np * jb.M; e += blockDim.x) {
+    const int i = e / jb.M, m = e - (e / jb.M) * jb.M;
+    const float* s = sm + i * jb.K;
+    float acc = jb.b ? jb.b[m] : 0.f;
+    for (int c = 0; c < jb.K; ++c) acc += s[c] * jb.wt[int64_t(c) * jb.M + m];
+    dst[e] = act_f(acc, jb.act);
   }
-  block_sync_global();
-  axial_attention(q, k, v, Lq, Lk, mid, a.d.heads, a.d.scale, y);
-  block_sync_global();
-  float* gate = (br == 0 ? a.ws.g1 + int64_t(n) * H * a.d.oup : a.ws.g2 + int64_t(n) * W * a.d.oup);
-  auto src_y = [&](int i, int m) { return y[int64_t(i) * mid + m]; };
-  proj(a.d.w[6 + br], a.d.b[6 + br], a.d.oup, mid, Lq, src_y, gate, 0);
 }
 
-// CoordAtt: one block per image.  y = SiLU(cv1(cat[x_h, x_w])) ; a_h = sigmoid(cv_h(y_h)) ; a_w = sigmoid(cv_w(y_w))
-__global__ __launch_bounds__(256) void coordatt_compute_kernel(CoordArgs a) {
-  const int n = blockIdx.x;
-  const int C = a.d.inp, H = a.H, W = a.W, mid = a.d.mid, YC = a.ws.YC;
-  float* y = a.ws.scratch + int64_t(n) * (H + W) * mid * 4;
-  const float* xh = a.ws.xh + int64_t(n) * H * C;
-  const float invH = 1.0f / (float)H;
-  auto src_cat = [&](int i, int c) {
-    return i < H ? xh[int64_t(i) * C + c] : xw_at(a.ws.colpart, n, YC, W, C, i - H, c, invH);
-  };
-  proj(a.d.w[0], a.d.b[0], mid, C, H + W, src_cat, y, 1);
-  block_sync_global();
-  auto src_yh = [&](int i, int m) { return y[int64_t(i) * mid + m]; };
-  auto src_yw = [&](int i, int m) { return y[int64_t(H + i) * mid + m]; };
-  float* ah = a.ws.g1 + int64_t(n) * H * a.d.oup;
-  float* aw = a.ws.g2 + int64_t(n) * W * a.d.oup;
-  proj(a.d.w[1], a.d.b[1], a.d.oup, mid, H, src_yh, ah, 0);
-  proj(a.d.w[2], a.d.b[2], a.d.oup, mid, W, src_yw, aw, 0);
-  block_sync_global();
-  for (int e = threadIdx.x; e < H * a.d.oup; e += blockDim.x) ah[e] = 1.0f / (1.0f + expf(-ah[e]));
-  for (int e = threadIdx.x; e < W * a.d.oup; e += blockDim.x) aw[e] = 1.0f / (1.0f + expf(-aw[e]));
+// ---------------------------------------------------------------------------- 3. attention + out proj
+struct AttJob {
+  const float* q;   // [N][Lq][mid]
+  const float* k;   // [N][Lk][mid]
+  const float* v;   // [N][Lk][mid]
+  const float* wt;  // [mid][oup]
+  const float* b;   // [oup]
+  float* dst;       // [N][Lq][oup]
+  int Lq, Lk, act;
+};
+struct AttArgs {
+  AttJob job[2];
+  int mid, heads, oup, QT;
+  float scale;
+};
+
+template <int DH>
+__global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const AttJob& jb = a.job[blockIdx.y];
+  const int n = blockIdx.z;
+  const int i0 = blockIdx.x * a.QT;
+  if (i0 >= jb.Lq) return;
+  const int mid = a.mid, Lk = jb.Lk;
+  float* ks = sm;                 // Lk*mid
+  float* vs = ks + Lk * mid;      // Lk*mid
+  float* ys = vs + Lk * mid;      // QT*mid
+  const float* kg = jb.k + int64_t(n) * Lk * mid;
+  const float* vg = jb.v + int64_t(n) * Lk * mid;
+  for (int e = threadIdx.x; e < Lk * mid; e += blockDim.x) {
+    ks[e] = kg[e];
+    vs[e] = vg[e];
+  }
+  __syncthreads();
+  const int nq = min(a.QT, jb.Lq - i0);
+  for (int e = threadIdx.x; e < nq * a.heads; e += blockDim.x) {
+    const int il = e / a.heads, hd = e - il * a.heads;
+    const float* qg = jb.q + (int64_t(n) * jb.Lq + i0 + il) * mid + hd * DH;
+    float q[DH], acc[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) {
+      q[d] = qg[d];
+      acc[d] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < Lk; ++j) {
+      const float* kj = ks + j * mid + hd * DH;
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) s += q[d] * kj[d];
+      s *= a.scale;
+      const float mn = fmaxf(m, s);
+      const float corr = expf(m - mn), p = expf(s - mn);
+      l = l * corr + p;
+      const float* vj = vs + j * mid + hd * DH;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[d] = acc[d] * corr + p * vj[d];
+      m = mn;
+    }
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) ys[il * mid + hd * DH + d] = acc[d] * inv;
+  }
+  __syncthreads();
+  float* dst = jb.dst + (int64_t(n) * jb.Lq + i0) * a.oup;
+  for (int e = threadIdx.x; e < nq * a.oup; e += blockDim.x) {
+    const int il = e / a.oup, c = e - il * a.oup;
+    const float* y = ys + il * mid;
+    float acc = jb.b ? jb.b[c] : 0.f;
+    for (int m2 = 0; m2 < mid; ++m2) acc += y[m2] * jb.wt[int64_t(m2) * a.oup + c];
+    dst[e] = act_f(acc, jb.act);
+  }
 }
 
-// CoordCrossAtt: one block per image.  y = cv1(cat) (no act); q = q_conv(y_h), k/v = k/v_conv(y_w);
-// z = softmax_W(q k^T * scale) v ; y_att = sigmoid(proj(z))  [H][oup]
-__global__ __launch_bounds__(256) void coordcross_compute_kernel(CoordArgs a) {
-  const int n = blockIdx.x;
-  const int C = a.d.inp, H = a.H, W = a.W, mid = a.d.mid, YC = a.ws.YC;
-  float* base = a.ws.scratch + int64_t(n) * (H + W) * mid * 4;
-  float* y = base;                       // (H+W) x mid
-  float* q = base + (H + W) * mid;       // H x mid
-  float* k = q + H * mid;                // W x mid
-  float* v = k + W * mid;                // W x mid
-  float* z = v + W * mid;                // H x mid  (fits: (H+W)*mid*4 >= (H+W)+H+2W+H)
-  const float* xh = a.ws.xh + int64_t(n) * H * C;
-  const float invH = 1.0f / (float)H;
-  auto src_cat = [&](int i, int c) {
-    return i < H ? xh[int64_t(i) * C + c] : xw_at(a.ws.colpart, n, YC, W, C, i - H, c, invH);
-  };
-  proj(a.d.w[0], a.d.b[0], mid, C, H + W, src_cat, y, 0);
-  block_sync_global();
-  auto src_yh = [&](int i, int m) { return y[int64_t(i) * mid + m]; };
-  auto src_yw = [&](int i, int m) { return y[int64_t(H + i) * mid + m]; };
-  proj(a.d.w[1], a.d.b[1], mid, mid, H, src_yh, q, 0);
-  proj(a.d.w[2], a.d.b[2], mid, mid, W, src_yw, k, 0);
-  proj(a.d.w[3], a.d.b[3], mid, mid, W, src_yw, v, 0);
-  block_sync_global();
-  axial_attention(q, k, v, H, W, mid, a.d.heads, a.d.scale, z);
-  block_sync_global();
-  float* g = a.ws.g1 + int64_t(n) * H * a.d.oup;
-  auto src_z = [&](int i, int m) { return z[int64_t(i) * mid + m]; };
-  proj(a.d.w[4], a.d.b[4], a.d.oup, mid, H, src_z, g, 0);
-  block_sync_global();
-  for (int e = threadIdx.x; e < H * a.d.oup; e += blockDim.x) g[e] = 1.0f / (1.0f + expf(-g[e]));
-}
-
-// ---------------------------------------------------------------------------- 3. apply
+// ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
 template <int MODE>
@@ -306,6 +263,50 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
 }
 
 // ---------------------------------------------------------------------------- host
+static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
+  ProjArgs pa;
+  int maxL = 1, maxK = 1;
+  for (int i = 0; i < nj; ++i) {
+    pa.job[i] = jobs[i];
+    maxL = std::max(maxL, jobs[i].L);
+    maxK = std::max(maxK, jobs[i].K);
+  }
+  const int TP = std::max(1, std::min(16, 8192 / maxK));
+  dim3 grid((maxL + TP - 1) / TP, nj, N);
+  hipLaunchKernelGGL(coord_proj_kernel, grid, dim3(256), size_t(TP) * maxK * sizeof(float), s, pa, TP);
+  return launch_status("coord_proj_kernel");
+}
+
+static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, hipStream_t s) {
+  AttArgs a;
+  a.mid = d.mid;
+  a.heads = d.heads;
+  a.oup = d.oup;
+  a.scale = d.scale;
+  a.QT = std::max(1, 256 / d.heads);
+  int maxLq = 1, maxLk = 1;
+  for (int i = 0; i < nj; ++i) {
+    a.job[i] = jobs[i];
+    maxLq = std::max(maxLq, jobs[i].Lq);
+    maxLk = std::max(maxLk, jobs[i].Lk);
+  }
+  const size_t shm = (size_t(2) * maxLk * d.mid + size_t(a.QT) * d.mid) * sizeof(float);
+  if (shm > 160 * 1024) return fail(FCE_ERR_UNSUPPORTED, "coord attention: K/V do not fit in LDS");
+  dim3 grid((maxLq + a.QT - 1) / a.QT, nj, N);
+  const int dh = d.mid / d.heads;
+  switch (dh) {
+#define ATT(DH) \
+  case DH:      \
+    hipLaunchKernelGGL(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a); break;
+    ATT(1) ATT(2) ATT(3) ATT(4) ATT(5) ATT(6) ATT(7) ATT(8) ATT(10) ATT(12) ATT(16) ATT(20) ATT(24) ATT(32)
+    ATT(48) ATT(64)
+#undef ATT
+    default:
+      return fail(FCE_ERR_UNSUPPORTED, "coord attention: unsupported head dim " + std::to_string(dh));
+  }
+  return launch_status("coord_attend_kernel");
+}
+
 static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, const fce_tensor& y, void* ws,
                         size_t ws_bytes, hipStream_t s) {
   FCE_CHECK(x.layout == FCE_NHWC && y.layout == FCE_NHWC && x.dtype == FCE_F16 && y.dtype == FCE_F16,
@@ -320,24 +321,46 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   const int N = x.n, H = x.h, W = x.w;
   if (int64_t(N) * H * W == 0) return FCE_OK;
   FCE_CHECK(ws && ws_bytes >= coord_ws_bytes(d, N, H, W), "coord attention: workspace too small");
-  CoordArgs a;
-  a.d = d;
-  a.H = H;
-  a.W = W;
-  ws_floats(kind, d, N, H, W, &a.ws, static_cast<float*>(ws));
+  CoordWs w;
+  ws_layout(d, N, H, W, &w, static_cast<float*>(ws));
   const _Float16* xp = static_cast<const _Float16*>(x.data) + x.coff;
-  hipLaunchKernelGGL(pool_rows_kernel, dim3(H, N), dim3(256), 0, s, xp, x.cstride, H, W, d.inp, a.ws.xh);
-  const int XW = 256 / (d.inp / 8);
-  hipLaunchKernelGGL(pool_cols_kernel, dim3((W + XW - 1) / XW, a.ws.YC, N), dim3(256), 0, s, xp, x.cstride, H, W,
-                     d.inp, a.ws.colpart, a.ws.YC);
-  if (kind == 0)
-    hipLaunchKernelGGL(bicoord_compute_kernel, dim3(N, 2), dim3(256), 0, s, a);
-  else if (kind == 1)
-    hipLaunchKernelGGL(coordatt_compute_kernel, dim3(N), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(coordcross_compute_kernel, dim3(N), dim3(256), 0, s, a);
-  int st = launch_status("coord compute");
+  const int C = d.inp, mid = d.mid;
+  hipLaunchKernelGGL(pool_rows_kernel, dim3(H, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh);
+  const int XW = 256 / (C / 8);
+  hipLaunchKernelGGL(pool_cols_kernel, dim3((W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xw);
+  int st = launch_status("coord pooling");
   if (st) return st;
+  if (kind == 0) {  // BiCoordCrossAtt
+    ProjJob pj[6] = {
+        {w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_NONE_},  // q_h  <- x_h
+        {w.xw, d.w[1], d.b[1], w.buf[1], W, C, mid, ACT_NONE_},  // k_h  <- x_w
+        {w.xw, d.w[2], d.b[2], w.buf[2], W, C, mid, ACT_NONE_},  // v_h  <- x_w
+        {w.xw, d.w[3], d.b[3], w.buf[3], W, C, mid, ACT_NONE_},  // q_w  <- x_w
+        {w.xh, d.w[4], d.b[4], w.buf[4], H, C, mid, ACT_NONE_},  // k_w  <- x_h
+        {w.xh, d.w[5], d.b[5], w.buf[5], H, C, mid, ACT_NONE_},  // v_w  <- x_h
+    };
+    if ((st = launch_proj(pj, 6, N, s))) return st;
+    AttJob aj[2] = {{w.buf[0], w.buf[1], w.buf[2], d.w[6], d.b[6], w.g1, H, W, ACT_NONE_},
+                    {w.buf[3], w.buf[4], w.buf[5], d.w[7], d.b[7], w.g2, W, H, ACT_NONE_}};
+    if ((st = launch_attend(aj, 2, N, d, s))) return st;
+  } else if (kind == 1) {  // CoordAtt: y = SiLU(cv1 [x_h; x_w]); a_h / a_w = sigmoid(cv_h / cv_w)
+    ProjJob p1[2] = {{w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_SILU_},
+                     {w.xw, d.w[0], d.b[0], w.buf[1], W, C, mid, ACT_SILU_}};
+    if ((st = launch_proj(p1, 2, N, s))) return st;
+    ProjJob p2[2] = {{w.buf[0], d.w[1], d.b[1], w.g1, H, mid, d.oup, ACT_SIGMOID_},
+                     {w.buf[1], d.w[2], d.b[2], w.g2, W, mid, d.oup, ACT_SIGMOID_}};
+    if ((st = launch_proj(p2, 2, N, s))) return st;
+  } else {  // CoordCrossAtt: y = cv1 [x_h; x_w]; q <- y_h, k,v <- y_w; y_att = sigmoid(proj(attn))
+    ProjJob p1[2] = {{w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_NONE_},
+                     {w.xw, d.w[0], d.b[0], w.buf[1], W, C, mid, ACT_NONE_}};
+    if ((st = launch_proj(p1, 2, N, s))) return st;
+    ProjJob p2[3] = {{w.buf[0], d.w[1], d.b[1], w.buf[2], H, mid, mid, ACT_NONE_},
+                     {w.buf[1], d.w[2], d.b[2], w.buf[3], W, mid, mid, ACT_NONE_},
+                     {w.buf[1], d.w[3], d.b[3], w.buf[4], W, mid, mid, ACT_NONE_}};
+    if ((st = launch_proj(p2, 3, N, s))) return st;
+    AttJob aj[1] = {{w.buf[2], w.buf[3], w.buf[4], d.w[4], d.b[4], w.g1, H, W, ACT_SIGMOID_}};
+    if ((st = launch_attend(aj, 1, N, d, s))) return st;
+  }
   // identity branch (1x1 conv with bias, no act) written into y first, then gated in place
   const _Float16* src = xp;
   int scs = x.cstride;
@@ -353,13 +376,13 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   const int blocks = int(std::min<int64_t>((total + 255) / 256, 65535 * 8));
   if (kind == 0)
     hipLaunchKernelGGL(gate_apply_kernel<GATE_BICOORD>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H,
-                       W, d.oup, a.ws.g1, a.ws.g2);
+                       W, d.oup, w.g1, w.g2);
   else if (kind == 1)
     hipLaunchKernelGGL(gate_apply_kernel<GATE_COORD>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H,
-                       W, d.oup, a.ws.g1, a.ws.g2);
+                       W, d.oup, w.g1, w.g2);
   else
     hipLaunchKernelGGL(gate_apply_kernel<GATE_ROW>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
-                       d.oup, a.ws.g1, a.ws.g2);
+                       d.oup, w.g1, w.g2);
   return launch_status("gate_apply_kernel");
 }
 

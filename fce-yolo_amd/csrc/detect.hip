@@ -33,14 +33,31 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs a) {
     const float* bx = L.box + (int64_t(n) * L.h * L.w + p) * L.bcs;
     float dist[4];
     for (int s = 0; s < 4; ++s) {
+      // same reduction tree as the fused conv epilogue (conv.hip OUT_DFL): four partial sums of
+      // 4 consecutive bins, combined as (g0 + g1) + (g2 + g3), so both paths agree bit for bit
       const float* b = bx + s * a.reg_max;
       float mx = -INFINITY;
       for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, b[i]);
       float den = 0.f, num = 0.f;
-      for (int i = 0; i < a.reg_max; ++i) {
-        const float e = expf(b[i] - mx);
-        den += e;
-        num += e * (float)i;
+      if (a.reg_max == 16) {
+        float sd[4], sn[4];
+        for (int g = 0; g < 4; ++g) {
+          sd[g] = 0.f;
+          sn[g] = 0.f;
+          for (int j = 0; j < 4; ++j) {
+            const float e = expf(b[g * 4 + j] - mx);
+            sd[g] += e;
+            sn[g] = __fadd_rn(sn[g], __fmul_rn(e, (float)(g * 4 + j)));  // no FMA: match the fused path
+          }
+        }
+        den = (sd[0] + sd[1]) + (sd[2] + sd[3]);
+        num = (sn[0] + sn[1]) + (sn[2] + sn[3]);
+      } else {
+        for (int i = 0; i < a.reg_max; ++i) {
+          const float e = expf(b[i] - mx);
+          den += e;
+          num += e * (float)i;
+        }
       }
       dist[s] = num / den;
     }

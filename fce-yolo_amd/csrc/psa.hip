@@ -2,85 +2,127 @@
 //   q,k,v = qkv.view(B, heads, 2*kd+hd, N).split([kd,kd,hd]) ;  out = v @ softmax(q^T k * kd^-0.5)^T + pe(v)
 // with pe = depthwise 3x3 (BN folded, no act) over v viewed as (B, heads*hd, H, W).
 // qkv is the NHWC fp16 output of the qkv 1x1 conv: channel (head*(2kd+hd) + r) is row r of that head.
-// One block = (image, head, 64 queries); K/V streamed through LDS in 64-key tiles with an online
-// (running max / sum) softmax in fp32; the pe term is added in the epilogue from the same v.
+//
+// pe(v) runs first through the depthwise-conv kernel (one launch per head on the v channel slice),
+// writing y; the attention kernel then adds its output into y.
+//
+// Attention = flash-style on MFMA (v_mfma_f32_16x16x32_f16), one block = (image, head, 64 queries),
+// one wave = 16 queries, K/V streamed in 64-key tiles:
+//   S^T[key][q] = K . Q^T     A = K rows (16 keys x 32 d, 16-byte loads), B = Q^T (one per wave)
+//                             -> each lane owns ONE query column (q = lane&15) and 4 keys per tile,
+//                                so the online softmax needs only two xor-shuffles (lanes ^16, ^32)
+//   O^T[d][q] += V^T . P^T     B = P^T straight from the S^T registers (cvt to f16): the MFMA's k
+//                             index is relabelled (slot j<4 -> key 4g+j, j>=4 -> key 16+4g+j-4) and
+//                             the A operand V^T is read from an LDS transpose of the V tile in that
+//                             same key order (two 8-byte LDS reads per fragment)
 #include "common.h"
 
 namespace fce {
 
+int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
+              const fce_tensor& y, hipStream_t s);
+
 template <int KD, int HD>
-__global__ __launch_bounds__(256) void psa_attention_kernel(const _Float16* qkv, int qcs, int H, int W, int heads,
-                                                            const float* pe_w, const float* pe_b, _Float16* y,
-                                                            int ycs, float scale) {
-  constexpr int QT = 64, KT = 64, DG = 4, DPT = HD / DG;
-  __shared__ float ks[KT][KD + 1];
-  __shared__ float vs[KT][HD + 4];
-  const int N = H * W;
+__global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
+                                                                 int ycs, float scale_log2) {
+  static_assert(KD == 32 && HD == 64, "C2PSA geometry");
+  constexpr int KT = 64, VTS = KT + 4;  // key tile, padded LDS row (conflict-free 8-byte reads)
+  __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VTS];
   const int n = blockIdx.z, hd = blockIdx.y;
-  const int t = threadIdx.x;
-  const int qi = t / DG, dg = t % DG;
-  const int tok = blockIdx.x * QT + qi;
-  const int hstride = 2 * KD + HD;
-  const _Float16* base = qkv + int64_t(n) * N * qcs + hd * hstride;
-  float q[KD];
-  const bool qok = tok < N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int q = blockIdx.x * 64 + wave * 16 + col;
+  const _Float16* base = qkv + int64_t(n) * N * qcs + hd * (2 * KD + HD);
+  // B operand Q^T: lane holds Q[q][8g..8g+7]
+  h8 qf = h8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (q < N) qf = *reinterpret_cast<const h8*>(base + int64_t(q) * qcs + 8 * g);
+  float m = -INFINITY, l = 0.f;
+  f4 acc[4];
 #pragma unroll
-  for (int d = 0; d < KD; ++d) q[d] = qok ? (float)base[int64_t(tok) * qcs + d] : 0.f;
-  float m = -INFINITY, l = 0.f, acc[DPT];
-#pragma unroll
-  for (int d = 0; d < DPT; ++d) acc[d] = 0.f;
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f4{0.f, 0.f, 0.f, 0.f};
+
   for (int k0 = 0; k0 < N; k0 += KT) {
     __syncthreads();
-    for (int e = t; e < KT * KD; e += 256) {
-      const int j = e / KD, d = e % KD;
-      ks[j][d] = (k0 + j < N) ? (float)base[int64_t(k0 + j) * qcs + KD + d] : 0.f;
+    // stage V tile transposed: vt[d][key]
+    for (int e = threadIdx.x; e < KT * (HD / 8); e += 256) {
+      const int key = e / (HD / 8), dc = (e % (HD / 8)) * 8;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 + key < N) v = *reinterpret_cast<const h8*>(base + int64_t(k0 + key) * qcs + 2 * KD + dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(dc + j) * VTS + key] = v[j];
     }
-    for (int e = t; e < KT * HD; e += 256) {
-      const int j = e / HD, d = e % HD;
-      vs[j][d] = (k0 + j < N) ? (float)base[int64_t(k0 + j) * qcs + 2 * KD + d] : 0.f;
+    // S^T tiles (16 keys each): A = K[key][8g..8g+7]
+    f4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int key = k0 + 16 * t + col;
+      h8 kf = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < N) kf = *reinterpret_cast<const h8*>(base + int64_t(key) * qcs + KD + 8 * g);
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
+    // online softmax over the 64 keys of this tile for query column q (log2 domain)
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + 16 * t + 4 * g + j;
+        const float v = key < N ? s[t][j] * scale_log2 : -INFINITY;
+        s[t][j] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16));
+    mt = fmaxf(mt, __shfl_xor(mt, 32));
+    const float mn = fmaxf(m, mt);
+    const float corr = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = exp2f(s[t][j] - mn);
+        s[t][j] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16);
+    rs += __shfl_xor(rs, 32);
+    l = l * corr + rs;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[dt][j] *= corr;
     __syncthreads();
-    const int kn = min(KT, N - k0);
-    for (int j = 0; j < kn; ++j) {
-      float s = 0.f;
+    // O^T += V^T P^T over two 32-key steps
 #pragma unroll
-      for (int d = 0; d < KD; ++d) s += q[d] * ks[j][d];
-      s *= scale;
-      const float mn = fmaxf(m, s);
-      const float corr = __expf(m - mn);
-      const float p = __expf(s - mn);
-      l = l * corr + p;
+    for (int u = 0; u < 2; ++u) {
+      h8 pf;
 #pragma unroll
-      for (int d = 0; d < DPT; ++d) acc[d] = acc[d] * corr + p * vs[j][dg * DPT + d];
-      m = mn;
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (_Float16)s[2 * u][j];
+        pf[j + 4] = (_Float16)s[2 * u + 1][j];
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const _Float16* row = vt + (16 * dt + col) * VTS + 32 * u + 4 * g;
+        const h4 lo = *reinterpret_cast<const h4*>(row);
+        const h4 hi = *reinterpret_cast<const h4*>(row + 16);
+        const h8 vf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, acc[dt], 0, 0, 0);
+      }
     }
   }
-  if (!qok) return;
+  if (q >= N) return;
   const float inv = 1.0f / l;
-  const int ty = tok / W, tx = tok % W;
-  const int c0 = hd * HD + dg * DPT;  // channel in the (B, heads*hd, H, W) view
-  float o[DPT];
+  _Float16* yo = y + (int64_t(n) * N + q) * ycs + hd * HD;
 #pragma unroll
-  for (int d = 0; d < DPT; ++d) o[d] = acc[d] * inv + pe_b[c0 + d];
-  for (int ky = -1; ky <= 1; ++ky) {
-    const int iy = ty + ky;
-    if (iy < 0 || iy >= H) continue;
-    for (int kx = -1; kx <= 1; ++kx) {
-      const int ix = tx + kx;
-      if (ix < 0 || ix >= W) continue;
-      const _Float16* vp = base + int64_t(iy * W + ix) * qcs + 2 * KD + dg * DPT;
-      const int tap = (ky + 1) * 3 + (kx + 1);
+  for (int dt = 0; dt < 4; ++dt) {
+    _Float16* p = yo + 16 * dt + 4 * g;
+    const h4 pe = *reinterpret_cast<const h4*>(p);  // pe(v) written by the depthwise pass
+    h4 o;
 #pragma unroll
-      for (int d = 0; d < DPT; ++d) o[d] += (float)vp[d] * pe_w[(c0 + d) * 9 + tap];
-    }
-  }
-  _Float16* yo = y + (int64_t(n) * N + tok) * ycs + c0;
-#pragma unroll
-  for (int d = 0; d < DPT; d += 8) {
-    h8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (_Float16)o[d + j];
-    *reinterpret_cast<h8*>(yo + d) = v;
+    for (int j = 0; j < 4; ++j) o[j] = (_Float16)((float)pe[j] + acc[dt][j] * inv);
+    *reinterpret_cast<h4*>(p) = o;
   }
 }
 
@@ -90,16 +132,29 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
             "psa_attention: NHWC f16 views");
   FCE_CHECK(qkv.c == heads * (2 * key_dim + head_dim) && y.c == heads * head_dim, "psa_attention: channel mismatch");
   FCE_CHECK(qkv.n == y.n && qkv.h == y.h && qkv.w == y.w, "psa_attention: shape mismatch");
-  FCE_CHECK(y.cstride % 8 == 0 && y.coff % 8 == 0, "psa_attention: 8-aligned output slice");
+  FCE_CHECK(y.cstride % 8 == 0 && y.coff % 8 == 0 && qkv.cstride % 8 == 0 && qkv.coff % 8 == 0,
+            "psa_attention: 8-aligned slices");
   if (!(key_dim == 32 && head_dim == 64))
     return fail(FCE_ERR_UNSUPPORTED, "psa_attention: only key_dim 32 / head_dim 64 (C2PSA, num_heads = c // 64)");
   const int N = qkv.h * qkv.w;
   if (N == 0 || qkv.n == 0) return FCE_OK;
+  // pe(v): depthwise 3x3 on each head's v slice -> y slice (the attention kernel accumulates on top)
+  for (int h = 0; h < heads; ++h) {
+    fce_tensor vx = qkv;
+    vx.c = head_dim;
+    vx.coff = qkv.coff + h * (2 * key_dim + head_dim) + 2 * key_dim;
+    fce_tensor vy = y;
+    vy.c = head_dim;
+    vy.coff = y.coff + h * head_dim;
+    const int st = dwconv3x3(vx, 1, pe_w + h * head_dim, heads * head_dim, pe_b + h * head_dim, 0, vy, s);
+    if (st) return st;
+  }
   dim3 grid((N + 63) / 64, heads, qkv.n);
-  hipLaunchKernelGGL((psa_attention_kernel<32, 64>), grid, dim3(256), 0, s,
-                     static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, qkv.h, qkv.w, heads, pe_w, pe_b,
-                     static_cast<_Float16*>(y.data) + y.coff, y.cstride, 1.0f / sqrtf((float)key_dim));
-  return launch_status("psa_attention_kernel");
+  const float scale_log2 = 1.4426950408889634f / sqrtf((float)key_dim);
+  hipLaunchKernelGGL((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
+                     static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
+                     static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
+  return launch_status("psa_attention_mfma_kernel");
 }
 
 }  // namespace fce

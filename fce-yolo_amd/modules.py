@@ -348,7 +348,7 @@ class Attention(nn.Module):
     def _pe(self, device):
         def build():
             w, b = fold_bn(self.pe.conv, getattr(self.pe, "bn", None))
-            return w.reshape(w.shape[0], 9).contiguous().to(device), b.contiguous().to(device)
+            return w.reshape(w.shape[0], 9).t().contiguous().to(device), b.contiguous().to(device)  # [9][C]
 
         return _cached(self.pe, device, build, "_fce_pe")
 
@@ -445,10 +445,10 @@ class BiFPN_Concat(nn.Module):
 
 
 def _dense(mod: nn.Conv2d, device):
-    """fp32 [out][in] matrix + bias of a 1x1 nn.Conv2d (device)."""
+    """fp32 transposed [in][out] matrix + bias of a 1x1 nn.Conv2d (device)."""
 
     def build():
-        w = mod.weight.detach().float().reshape(mod.out_channels, -1).contiguous().to(device)
+        w = mod.weight.detach().float().reshape(mod.out_channels, -1).t().contiguous().to(device)
         b = (mod.bias.detach().float() if mod.bias is not None else torch.zeros(mod.out_channels)).to(device)
         return w, b.contiguous()
 
@@ -485,7 +485,7 @@ class CoordAtt(nn.Module):
 
         def build():
             w, b = fold_bn(self.cv1.conv, getattr(self.cv1, "bn", None))
-            return w.reshape(mip, inp).contiguous().to(be.device), b.contiguous().to(be.device)
+            return w.reshape(mip, inp).t().contiguous().to(be.device), b.contiguous().to(be.device)
 
         cv1 = _cached(self.cv1, be.device, build, "_fce_cv1")
         d = _coord_desc(inp, oup, mip, 1, 1.0, [cv1, _dense(self.cv_h, be.device), _dense(self.cv_w, be.device)],
@@ -619,25 +619,48 @@ class Detect(nn.Module):
             raise RuntimeError("Detect.stride is not set (DetectionModel sets [8, 16, 32])")
         return s
 
-    def emit_maps(self, be, xs):
-        maps = []
-        for i, x in enumerate(xs):
-            mp = be.alloc(x.n, self.no, x.h, x.w, N.F32)  # cat(box, cls) (head.py:122), fp32 logits (Q11)
-            b = self.cv2[i][1].emit(be, self.cv2[i][0].emit(be, x))
-            emit_conv(be, self.cv2[i][2], None, False, b, out=mp.slice(0, 4 * self.reg_max))
-            seq = self.cv3[i]
-            if self.legacy:
-                c = seq[1].emit(be, seq[0].emit(be, x))
-            else:
-                c = seq[0][1].emit(be, seq[0][0].emit(be, x))
-                c = seq[1][1].emit(be, seq[1][0].emit(be, c))
-            emit_conv(be, seq[2], None, False, c, out=mp.slice(4 * self.reg_max, self.nc))
-            maps.append(mp)
-        return maps
+    def _branches(self, be, x, i):
+        """Features feeding the last 1x1 convs of level i: (box branch, cls branch)."""
+        b = self.cv2[i][1].emit(be, self.cv2[i][0].emit(be, x))
+        seq = self.cv3[i]
+        if self.legacy:
+            c = seq[1].emit(be, seq[0].emit(be, x))
+        else:
+            c = seq[0][1].emit(be, seq[0][0].emit(be, x))
+            c = seq[1][1].emit(be, seq[1][0].emit(be, c))
+        return b, c
+
+    def _finals(self, i):
+        return ((0, self.cv2[i][2]), (1, self.cv3[i][2]))
 
     def emit(self, be, xs, out=None):
-        maps = self.emit_maps(be, xs)
-        pred = be.detect(maps, self.strides(), self.reg_max)
+        """Graph backend: the box / cls logits never leave the last convs (fp32 DFL decode + sigmoid in
+        the epilogue, written straight into pred).  Eager backend: the same fused kernels produce pred
+        (bit-identical to the graph path) and fp32 raw maps are also written for the reference's
+        ``(y, x)`` return (head.py:122-124)."""
+        strides = self.strides()
+        fused_only = getattr(be, "fused_detect", False)
+        pred, maps = None, []
+        if not fused_only:
+            A = sum(v.h * v.w for v in xs)
+            pred = torch.empty((xs[0].n, 4 + self.nc, A), dtype=torch.float32, device=be.device)
+        off = 0
+        for i, x in enumerate(xs):
+            feats = self._branches(be, x, i)
+            if not fused_only:
+                mp = be.alloc(x.n, self.no, x.h, x.w, N.F32)  # cat(box, cls) raw logits, fp32
+                emit_conv(be, self.cv2[i][2], None, False, feats[0], out=mp.slice(0, 4 * self.reg_max))
+                emit_conv(be, self.cv3[i][2], None, False, feats[1], out=mp.slice(4 * self.reg_max, self.nc))
+                maps.append(mp)
+            for (part, conv), v in zip(self._finals(i), feats):
+                nat = conv_native(conv, None, False, be.device)
+                if fused_only:
+                    be.conv_detect(nat.desc, v, part, i, strides[i], self.nc, self.reg_max, nat.w.data_ptr(),
+                                   nat.b.data_ptr())
+                else:
+                    be.conv_detect(nat.desc, v, pred, A, off, part, strides[i], self.nc, self.reg_max,
+                                   nat.w.data_ptr(), nat.b.data_ptr())
+            off += x.h * x.w
         return pred, maps
 
     def forward(self, x):

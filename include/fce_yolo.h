@@ -94,6 +94,18 @@ int fce_conv_pack_weights(const fce_conv_desc* d, const float* w_oihw, void* pac
 int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
                const fce_tensor* residual, const fce_tensor* y, void* stream);
 
+/* Detect tail fused into the last 1x1 conv of a branch (head.py:149-167): part 0 = box branch
+ * (4*reg_max logits -> DFL expectation -> xywh * stride into pred rows 0..3), part 1 = cls branch
+ * (nc logits -> sigmoid into pred rows 4..).  pred: (N, 4+nc, anchors) fp32; this level's anchors
+ * start at anchor_offset. */
+typedef struct fce_detect_epi {
+  float* pred;
+  int anchors, anchor_offset, nc, reg_max, part;
+  float stride;
+} fce_detect_epi;
+int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
+                      const fce_detect_epi* e, void* stream);
+
 /* ---------------------------------------------------------------- pooling / fusion */
 /* SPPF chain: y1 = maxpool_k(x), y2 = maxpool_k(y1), y3 = maxpool_k(y2), stride 1, -inf pad. */
 int fce_maxpool_chain(const fce_tensor* x, const fce_tensor* y1, const fce_tensor* y2, const fce_tensor* y3, int k,
@@ -106,11 +118,11 @@ int fce_weighted_add(const fce_tensor* x, int up, const float* fusion_w, int fus
 typedef struct fce_coord_desc {
   int inp, oup, mid, heads; /* mid = dim_head*heads (BiCoord) / mip (CoordAtt, CoordCrossAtt) */
   float scale;              /* softmax scale                                                  */
-  /* fp32 device weights, row-major [out][in]; biases [out].  Usage per op:
-   *   BiCoordCrossAtt: w[0..5] = proj_q_h, proj_k_h, proj_v_h, proj_q_w, proj_k_w, proj_v_w (mid x inp),
-   *                    w[6] = out_h, w[7] = out_w (oup x mid)
-   *   CoordAtt:        w[0] = cv1 (mid x inp, BN folded, SiLU), w[1] = cv_h, w[2] = cv_w (oup x mid)
-   *   CoordCrossAtt:   w[0] = cv1 (mid x inp), w[1..3] = q_conv, k_conv, v_conv (mid x mid), w[4] = proj */
+  /* fp32 device weights of the 1x1 convs, TRANSPOSED: [in][out] row-major; biases [out].  Usage:
+   *   BiCoordCrossAtt: w[0..5] = proj_q_h, proj_k_h, proj_v_h, proj_q_w, proj_k_w, proj_v_w (inp x mid),
+   *                    w[6] = out_h, w[7] = out_w (mid x oup)
+   *   CoordAtt:        w[0] = cv1 (inp x mid, BN folded, SiLU), w[1] = cv_h, w[2] = cv_w (mid x oup)
+   *   CoordCrossAtt:   w[0] = cv1 (inp x mid), w[1..3] = q_conv, k_conv, v_conv (mid x mid), w[4] = proj */
   const float* w[8];
   const float* b[8];
   /* identity 1x1 conv when inp != oup (packed with fce_conv_pack_weights), else NULL */
@@ -129,7 +141,9 @@ int fce_coordcrossatt(const fce_coord_desc* d, const fce_tensor* x, const fce_te
 /* ---------------------------------------------------------------- C2PSA attention */
 /* qkv: NHWC f16 with heads*(2*key_dim+head_dim) channels ([q|k|v] per head, block.py:1296);
  * y: NHWC f16 with heads*head_dim channels = softmax(q^T k * key_dim^-0.5) v + pe(v);
- * pe_w: (heads*head_dim) x 9 fp32 depthwise taps (BN folded), pe_b: fp32. */
+ * pe_w: 9 x (heads*head_dim) fp32 depthwise taps, BN folded — the layout fce_conv_pack_weights
+ * produces for the depthwise desc (tap-major); pe_b: fp32 (heads*head_dim).
+ * Only key_dim 32 / head_dim 64 (C2PSA: num_heads = c // 64, attn_ratio 0.5). */
 int fce_psa_attention(const fce_tensor* qkv, int heads, int key_dim, int head_dim, const float* pe_w,
                       const float* pe_b, const fce_tensor* y, void* stream);
 
@@ -170,6 +184,10 @@ int fce_net_add_psa_attention(fce_net* net, int qkv_buf, int heads, int key_dim,
                               const float* pe_b, int out_buf, int out_coff);
 /* map_bufs[i]: f32 buffer of level i holding cat(box 4*reg_max, cls nc) channels (head.py:122) */
 int fce_net_add_detect(fce_net* net, int nl, const int* map_bufs, const float* strides, int reg_max);
+/* Fused Detect tail conv (see fce_conv2d_detect) writing the forward's pred output; `level` orders
+ * the anchor blocks (offsets are resolved at plan time). */
+int fce_net_add_conv_detect(fce_net* net, const fce_conv_desc* d, int in_buf, int in_coff, int part, int level,
+                            float stride, int nc, int reg_max, const void* w_packed, const float* bias);
 /* allocate the arena for (batch, H, W); invalidates any captured graph */
 int fce_net_plan(fce_net* net, int batch, int h, int w);
 size_t fce_net_arena_bytes(const fce_net* net);

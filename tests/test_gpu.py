@@ -86,6 +86,17 @@ def test_detect_parity(ops_fx, device):
     assert (y[:, 4:].cpu() - ref[:, 4:]).abs().max().item() <= CLS_TOL * 3
     for i in range(3):
         assert _rel(maps[i], torch.from_numpy(fx[f"map{i}"])) <= OP_TOL
+    # the standalone decode kernel (fce_detect_decode) on the reference's own fp32 maps
+    from fce_yolo_amd.backend import EagerBackend, View
+
+    be = EagerBackend(device)
+    views = []
+    for i in range(3):
+        m = torch.from_numpy(fx[f"map{i}"]).to(device).contiguous(memory_format=torch.channels_last)
+        views.append(View(m, m.shape[0], m.shape[1], m.shape[2], m.shape[3], m.shape[1], 0, N.F32))
+    yd = be.detect(views, [8.0, 16.0, 32.0], 16)
+    assert _rel(yd[:, :4], ref[:, :4]) <= 1e-6
+    assert (yd[:, 4:].cpu() - ref[:, 4:]).abs().max().item() <= 1e-6
 
 
 def _engine_run(key, fx, device, graph=True):
