@@ -364,46 +364,69 @@ struct DwArgs {
   int act;
 };
 
+// One thread = PX adjacent output pixels x 8 channels: the 9 tap weights are loaded once and the
+// S*(PX-1)+3 input columns of each row are shared by the PX outputs.
+template <int S, int PX>
 __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
+  constexpr int NCOL = S * (PX - 1) + 3;
   const int cg8 = a.C >> 3;
+  const int Q = (a.Wo + PX - 1) / PX;
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= a.Wo * cg8) return;
-  const int ox = idx / cg8, c0 = (idx - ox * cg8) * 8;
+  if (idx >= Q * cg8) return;
+  const int q = idx / cg8, c0 = (idx - q * cg8) * 8;
   const int row = blockIdx.y, n = row / a.Ho, oy = row - n * a.Ho;
-  float acc[8];
+  const int ox0 = q * PX, ix0 = ox0 * S - 1;
+  float wk[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const f4 w0 = *reinterpret_cast<const f4*>(a.w + t * a.wcs + c0);
+    const f4 w1 = *reinterpret_cast<const f4*>(a.w + t * a.wcs + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wk[t][j] = w0[j];
+      wk[t][j + 4] = w1[j];
+    }
+  }
+  float acc[PX][8];
   {
     const f4 b0 = *reinterpret_cast<const f4*>(a.bias + c0);
     const f4 b1 = *reinterpret_cast<const f4*>(a.bias + c0 + 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[j] = b0[j];
-      acc[j + 4] = b1[j];
-    }
+    for (int p = 0; p < PX; ++p)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[p][j] = b0[j];
+        acc[p][j + 4] = b1[j];
+      }
   }
   const _Float16* xn = a.x + int64_t(n) * a.H * a.W * a.xcs + c0;
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky) {
-    const int iy = oy * a.stride - 1 + ky;
+    const int iy = oy * S - 1 + ky;
     if (iy < 0 || iy >= a.H) continue;
+    const _Float16* xr = xn + int64_t(iy) * a.W * a.xcs;
+    h8 v[NCOL];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = ox * a.stride - 1 + kx;
-      if (ix < 0 || ix >= a.W) continue;
-      const h8 v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix) * a.xcs);
-      const float* wt = a.w + (ky * 3 + kx) * a.wcs + c0;
-      const f4 w0 = *reinterpret_cast<const f4*>(wt);
-      const f4 w1 = *reinterpret_cast<const f4*>(wt + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] += (float)v[j] * w0[j];
-        acc[j + 4] += (float)v[j + 4] * w1[j];
-      }
+    for (int c = 0; c < NCOL; ++c) {
+      const int ix = ix0 + c;
+      v[c] = (ix >= 0 && ix < a.W) ? *reinterpret_cast<const h8*>(xr + int64_t(ix) * a.xcs)
+                                   : h8{0, 0, 0, 0, 0, 0, 0, 0};
     }
-  }
-  h8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
-  *reinterpret_cast<h8*>(a.y + (int64_t(row) * a.Wo + ox) * a.ycs + c0) = o;
+    for (int p = 0; p < PX; ++p)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[p][j] += (float)v[p * S + kx][j] * wk[ky * 3 + kx][j];
+  }
+#pragma unroll
+  for (int p = 0; p < PX; ++p) {
+    if (ox0 + p >= a.Wo) break;
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[p][j]) : acc[p][j]);
+    *reinterpret_cast<h8*>(a.y + (int64_t(row) * a.Wo + ox0 + p) * a.ycs + c0) = o;
+  }
 }
 
 // depthwise 3x3 (pad 1) on NHWC f16 slices; w = [9][wcs] fp32 taps (BN folded), bias fp32 [C]
@@ -420,8 +443,12 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
   FCE_CHECK(int64_t(y.n) * Ho < 65536 * 1024, "dwconv: too many output rows");
   DwArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.n, x.h, x.w, x.cstride, x.c, stride, Ho, Wo,
            w, wcs, bias, static_cast<_Float16*>(y.data) + y.coff, y.cstride, act};
-  dim3 grid((Wo * (x.c / 8) + 255) / 256, y.n * Ho);
-  hipLaunchKernelGGL(dwconv_kernel, grid, dim3(256), 0, s, a);
+  constexpr int PX = 4;
+  dim3 grid(((Wo + PX - 1) / PX * (x.c / 8) + 255) / 256, y.n * Ho);
+  if (stride == 1)
+    hipLaunchKernelGGL((dwconv_kernel<1, PX>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((dwconv_kernel<2, PX>), grid, dim3(256), 0, s, a);
   return launch_status("dwconv_kernel");
 }
 
@@ -498,6 +525,92 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
         const int co = co0 + j;
         const float t = acc[co] + (co < a.cout ? a.bias[co] : 0.f);
         o[j] = (_Float16)(a.act ? silu(t) : t);
+      }
+      *reinterpret_cast<h8*>(yo + co0) = o;
+    }
+  }
+}
+
+// 3x3 stride-2 stem (the network's first Conv, 640 -> 320): one thread = PX adjacent output pixels
+// of one row.  Their receptive columns are the aligned run x[2*PX*q .. 2*PX*q + 2PX-1] plus the
+// element before it, so each (ci, ky) costs one vector load + one scalar load instead of 3*PX.
+// Weights [ci][ky][kx][co] broadcast from LDS; same per-pixel summation order as stem_kernel.
+template <typename T, int NE>
+__device__ __forceinline__ void load_run(const T* p, float* out) {
+  T tmp[NE];
+  __builtin_memcpy(tmp, __builtin_assume_aligned(p, sizeof(T) * NE), sizeof(T) * NE);
+#pragma unroll
+  for (int e = 0; e < NE; ++e) out[e] = ld_in<T>(tmp, e);
+}
+
+template <int COUT, int PX, typename T>
+__global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nw = a.C * 9 * COUT;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    const int co = i % COUT, r = i / COUT;
+    smem[i] = co < a.cout ? a.w[r * a.cout + co] : 0.f;
+  }
+  __syncthreads();
+  const int Q = (a.Wo + PX - 1) / PX;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int row = idx / Q, q = idx - row * Q;
+  if (row >= a.N * a.Ho) return;
+  const int n = row / a.Ho, oy = row - n * a.Ho;
+  const int ix0 = 2 * PX * q;
+  const T* x = static_cast<const T*>(a.x);
+  float acc[PX][COUT];
+#pragma unroll
+  for (int j = 0; j < PX; ++j)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[j][co] = 0.f;
+  for (int ci = 0; ci < a.C; ++ci) {
+    const T* plane = x + (int64_t(n) * a.C + ci) * a.H * a.W;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = 2 * oy - 1 + ky;
+      if (iy < 0 || iy >= a.H) continue;
+      const T* rp = plane + int64_t(iy) * a.W;
+      float v[2 * PX + 1];
+      v[0] = ix0 > 0 ? ld_in<T>(rp, ix0 - 1) : 0.f;
+      if (ix0 + 2 * PX <= a.W) {
+        load_run<T, 2 * PX>(rp + ix0, v + 1);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 2 * PX; ++e) v[1 + e] = ix0 + e < a.W ? ld_in<T>(rp, ix0 + e) : 0.f;
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float* wt = smem + ((ci * 3 + ky) * 3 + kx) * COUT;
+#pragma unroll
+        for (int co = 0; co < COUT; co += 4) {
+          const f4 w4 = *reinterpret_cast<const f4*>(wt + co);
+#pragma unroll
+          for (int j = 0; j < PX; ++j) {
+            const float xv = v[2 * j + kx];
+            acc[j][co] += xv * w4[0];
+            acc[j][co + 1] += xv * w4[1];
+            acc[j][co + 2] += xv * w4[2];
+            acc[j][co + 3] += xv * w4[3];
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const int ox = PX * q + j;
+    if (ox >= a.Wo) break;
+    _Float16* yo = a.y + (int64_t(row) * a.Wo + ox) * a.ycs;
+#pragma unroll
+    for (int co0 = 0; co0 < COUT; co0 += 8) {
+      if (co0 >= a.cout) break;
+      h8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = co0 + e;
+        const float t = acc[j][co] + (co < a.cout ? a.bias[co] : 0.f);
+        o[e] = (_Float16)(a.act ? silu(t) : t);
       }
       *reinterpret_cast<h8*>(yo + co0) = o;
     }
@@ -609,6 +722,33 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     int coutT = d.cout <= 16 ? 16 : d.cout <= 32 ? 32 : d.cout <= 64 ? 64 : d.cout <= 96 ? 96 : 0;
     FCE_CHECK(coutT > 0, "stem conv: cout > 96 unsupported");
     const size_t shm = size_t(x.c) * d.k * d.k * coutT * sizeof(float);
+    const int PX = coutT <= 16 ? 4 : coutT <= 32 ? 2 : 1;
+    if (d.k == 3 && d.stride == 2 && x.w % (2 * PX) == 0) {
+      const int64_t threads = int64_t(x.n) * Ho * ((Wo + PX - 1) / PX);
+      FCE_CHECK(threads < (int64_t(1) << 31), "stem conv: input too large");
+      const dim3 grid(unsigned((threads + 255) / 256));
+#define STEM2_LAUNCH(CT, P, T) hipLaunchKernelGGL((stem_s2_kernel<CT, P, T>), grid, dim3(256), shm, s, a)
+#define STEM2_DT(CT, P)                  \
+  do {                                   \
+    if (x.dtype == FCE_F16)              \
+      STEM2_LAUNCH(CT, P, _Float16);     \
+    else if (x.dtype == FCE_F32)         \
+      STEM2_LAUNCH(CT, P, float);        \
+    else                                 \
+      STEM2_LAUNCH(CT, P, uint8_t);      \
+  } while (0)
+      if (coutT == 16)
+        STEM2_DT(16, 4);
+      else if (coutT == 32)
+        STEM2_DT(32, 2);
+      else if (coutT == 64)
+        STEM2_DT(64, 1);
+      else
+        STEM2_DT(96, 1);
+#undef STEM2_DT
+#undef STEM2_LAUNCH
+      return launch_status("stem_s2_kernel");
+    }
 #define STEM_LAUNCH(CT, T) hipLaunchKernelGGL((stem_kernel<CT, T>), dim3(blocks), dim3(256), shm, s, a)
 #define STEM_DT(CT)                      \
   do {                                   \

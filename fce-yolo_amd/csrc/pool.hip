@@ -70,6 +70,71 @@ __global__ __launch_bounds__(256) void maxpool_chain_kernel(MpArgs a) {
   }
 }
 
+// LDS-plane variant (the SPPF map is the stride-32 one: 20x20 at 640): one block per (image,
+// 8-channel group) holds the whole H x W plane in LDS, takes row maxima over radii r/2r/3r
+// (13 LDS reads), then column maxima of those (5+9+13 reads).  fp16 max is exact, so the result
+// equals the window max of the direct kernel bit for bit.
+__device__ __forceinline__ h8 hmax8(h8 a, h8 b) { return __builtin_elementwise_max(a, b); }
+
+__global__ __launch_bounds__(256) void maxpool_chain_lds_kernel(MpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) h8 pl[];
+  const int HW = a.H * a.W, cg = a.C >> 3;
+  const int n = blockIdx.x / cg, g = blockIdx.x - n * cg;
+  h8* xs = pl;
+  h8* r1 = pl + HW;
+  h8* r2 = pl + 2 * HW;
+  h8* r3 = pl + 3 * HW;
+  const _Float16* xb = a.x + int64_t(n) * HW * a.xcs + g * 8;
+  for (int p = threadIdx.x; p < HW; p += 256) xs[p] = *reinterpret_cast<const h8*>(xb + int64_t(p) * a.xcs);
+  __syncthreads();
+  const int r = a.r;
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const int y = p / a.W, x = p - y * a.W;
+    const h8* row = xs + y * a.W;
+    h8 m1 = row[x], m2, m3;
+    for (int d = 1; d <= r; ++d) {
+      if (x - d >= 0) m1 = hmax8(m1, row[x - d]);
+      if (x + d < a.W) m1 = hmax8(m1, row[x + d]);
+    }
+    m2 = m1;
+    for (int d = r + 1; d <= 2 * r; ++d) {
+      if (x - d >= 0) m2 = hmax8(m2, row[x - d]);
+      if (x + d < a.W) m2 = hmax8(m2, row[x + d]);
+    }
+    m3 = m2;
+    for (int d = 2 * r + 1; d <= 3 * r; ++d) {
+      if (x - d >= 0) m3 = hmax8(m3, row[x - d]);
+      if (x + d < a.W) m3 = hmax8(m3, row[x + d]);
+    }
+    r1[p] = m1;
+    r2[p] = m2;
+    r3[p] = m3;
+  }
+  __syncthreads();
+  const int64_t pix0 = int64_t(n) * HW;
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const int y = p / a.W, x = p - y * a.W;
+    h8 m1 = r1[p], m2 = r2[p], m3 = r3[p];
+    for (int d = 1; d <= 3 * r; ++d) {
+      const int yu = y - d, yd = y + d;
+      if (d <= r) {
+        if (yu >= 0) m1 = hmax8(m1, r1[yu * a.W + x]);
+        if (yd < a.H) m1 = hmax8(m1, r1[yd * a.W + x]);
+      }
+      if (d <= 2 * r) {
+        if (yu >= 0) m2 = hmax8(m2, r2[yu * a.W + x]);
+        if (yd < a.H) m2 = hmax8(m2, r2[yd * a.W + x]);
+      }
+      if (yu >= 0) m3 = hmax8(m3, r3[yu * a.W + x]);
+      if (yd < a.H) m3 = hmax8(m3, r3[yd * a.W + x]);
+    }
+    const int64_t pix = pix0 + p;
+    *reinterpret_cast<h8*>(a.y1 + pix * a.y1cs + g * 8) = m1;
+    *reinterpret_cast<h8*>(a.y2 + pix * a.y2cs + g * 8) = m2;
+    *reinterpret_cast<h8*>(a.y3 + pix * a.y3cs + g * 8) = m3;
+  }
+}
+
 int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
                   hipStream_t s) {
   for (const fce_tensor* t : {&x, &y1, &y2, &y3}) {
@@ -84,6 +149,11 @@ int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y
            x.n, x.h, x.w, x.c, k / 2};
   const int64_t total = int64_t(x.n) * x.h * x.w * (x.c / 8);
   if (total == 0) return FCE_OK;
+  const size_t lds = size_t(4) * x.h * x.w * sizeof(h8);
+  if (lds <= 64 * 1024 && int64_t(x.n) * (x.c / 8) < (int64_t(1) << 31)) {  // H*W <= 1024 (imgsz <= 1024)
+    hipLaunchKernelGGL(maxpool_chain_lds_kernel, dim3(x.n * (x.c / 8)), dim3(256), lds, s, a);
+    return launch_status("maxpool_chain_lds_kernel");
+  }
   int blocks = int(std::min<int64_t>((total + 255) / 256, 65535 * 8));
   hipLaunchKernelGGL(maxpool_chain_kernel, dim3(blocks), dim3(256), 0, s, a);
   return launch_status("maxpool_chain_kernel");
