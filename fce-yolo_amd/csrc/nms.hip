@@ -130,10 +130,6 @@ __device__ __forceinline__ float iou_ref(float4 bi, float ai, float4 bj, float a
   return inter / ((ai + aj) - inter);
 }
 
-__device__ __forceinline__ float4 shfl4(float4 v, int src) {
-  return make_float4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
-}
-
 // best class per anchor (first maximum, like torch.max): one thread per (image, anchor), all CUs
 __global__ __launch_bounds__(256) void nms_best_class_kernel(const float* pred, int nc, int A, int max_nms, char* ws,
                                                              size_t ws_per_image) {
@@ -179,6 +175,9 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
   __shared__ int tile_idx[TILE];
   __shared__ float4 tile_box[TILE];
   __shared__ float tile_area[TILE];
+  __shared__ uint64_t tile_sup[TILE];
+  __shared__ float4 kept_box[TILE];
+  __shared__ float kept_area[TILE];
   __shared__ int s_total, s_tile_n, s_next, s_nk, s_done, s_kept;
 
   const int n = blockIdx.x;
@@ -260,11 +259,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
   };
 
   if (!degenerate) {
-    // ---- 4a. tiled greedy (exact when every area > 0)
+    // ---- 4a. tiled greedy (exact when every area > 0).  Per tile of the next 64 surviving
+    // candidates: (i) wave 0 gathers them; (ii) all 16 waves build the tile's suppression rows
+    // sup[t] = {u > t : IoU(t, u) > thr} with one ballot each; (iii) wave 0 resolves the greedy
+    // order with 64-bit mask operations; (iv) every later candidate is tested against the kept
+    // members in parallel.
     int cursor = 0;
     while (true) {
       if (wv == 0) {
-        int cnt = 0, c = cursor, next = M;
+        int cnt = 0, c = cursor;
         while (cnt < TILE && c < M) {
           const int j = c + lane;
           const bool alive = j < M && !lremoved[j];
@@ -278,42 +281,57 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile_idx writes have landed
         __builtin_amdgcn_wave_barrier();
-        // resolve the tile sequentially inside this wave
-        const bool have = lane < cnt;
-        const int my = have ? tile_idx[lane] : 0;
-        if (cnt == TILE) next = __shfl(my, TILE - 1) + 1;  // resume right after the last tile member
-        float4 mb = have ? obox[my] : make_float4(0, 0, 0, 0);
-        float ma = have ? area[my] : 0.f;
-        bool rem = !have;
-        int kept0 = s_kept, nk = 0;
+        if (lane < cnt) {
+          const int my = tile_idx[lane];
+          tile_box[lane] = obox[my];
+          tile_area[lane] = area[my];
+        }
+        if (lane == 0) {
+          s_tile_n = cnt;
+          s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : M;  // resume right after the last member
+        }
+      }
+      __syncthreads();
+      const int cnt = s_tile_n;
+      if (cnt == 0) break;
+      for (int t = wv; t < cnt; t += NMS_THREADS / 64) {
+        bool sup = false;
+        if (lane > t && lane < cnt) {
+          float inter;
+          sup = iou_ref(tile_box[t], tile_area[t], tile_box[lane], tile_area[lane], &inter) > iou_thres;
+        }
+        const uint64_t b = __ballot(sup);
+        if (lane == 0) tile_sup[t] = b;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        const int kept0 = s_kept;
+        const uint64_t mysup = lane < cnt ? tile_sup[lane] : 0ull;
+        const uint32_t sup_lo = uint32_t(mysup), sup_hi = uint32_t(mysup >> 32);
+        uint64_t removed = 0, keptm = 0;
+        int nk = 0;
         bool done = false;
-        for (int t = 0; t < cnt; ++t) {
-          const bool rt = __shfl(rem ? 1 : 0, t) != 0;
-          if (rt) continue;
-          const float4 bt = shfl4(mb, t);
-          const float at = __shfl(ma, t);
-          if (lane == t) {
-            tile_box[nk] = mb;
-            tile_area[nk] = ma;
-            emit_det(my, kept0 + nk);
-          }
+        for (int t = 0; t < cnt; ++t) {  // wave-uniform: SALU bit ops + v_readlane
+          if ((removed >> t) & 1ull) continue;
+          keptm |= 1ull << t;
           ++nk;
           if (kept0 + nk >= max_det) {
             done = true;
             break;
           }
-          if (lane > t && !rem) {
-            float inter;
-            const float iou = iou_ref(bt, at, mb, ma, &inter);
-            if (iou > iou_thres) rem = true;
-          }
+          removed |= uint64_t(__builtin_amdgcn_readlane(sup_lo, t)) |
+                     (uint64_t(__builtin_amdgcn_readlane(sup_hi, t)) << 32);
+        }
+        if ((keptm >> lane) & 1ull) {
+          const int r = __popcll(keptm & ((1ull << lane) - 1ull));
+          kept_box[r] = tile_box[lane];
+          kept_area[r] = tile_area[lane];
+          emit_det(tile_idx[lane], kept0 + r);
         }
         if (lane == 0) {
-          s_tile_n = cnt;
-          s_next = next;
           s_nk = nk;
           s_kept = kept0 + nk;
-          s_done = done || cnt == 0 || next >= M;
+          s_done = done || s_next >= M;
         }
       }
       __syncthreads();
@@ -326,7 +344,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
         const float aj = area[j];
         for (int k = 0; k < nk; ++k) {
           float inter;
-          if (iou_ref(tile_box[k], tile_area[k], bj, aj, &inter) > iou_thres) {
+          if (iou_ref(kept_box[k], kept_area[k], bj, aj, &inter) > iou_thres) {
             lremoved[j] = 1;
             break;
           }
