@@ -29,6 +29,7 @@ sys.path.insert(0, str(ROOT))
 import fce_pkg  # noqa: E402
 
 fce_pkg.load()
+from fce_yolo_amd.dist import broadcast_module  # noqa: E402
 from fce_yolo_amd.engine import NMS, Engine  # noqa: E402
 from fce_yolo_amd.parser import DetectionModel  # noqa: E402
 from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
@@ -99,9 +100,7 @@ def main():
         model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
     model.eval().to(dev)
     if world > 1:  # weights broadcast once per model load (RCCL over xGMI)
-        with torch.no_grad():
-            for t in list(model.parameters()) + list(model.buffers()):
-                dist.broadcast(t.data, src=0)
+        broadcast_module(model, src=0)
 
     B, S = a.batch, a.imgsz
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)

@@ -1,18 +1,23 @@
 // Non-maximum suppression on the device (reference ultralytics/utils/nms.py:13-166 with the predict
 // defaults multi_label=False, agnostic=False, classes=None; TorchNMS.nms :239-296; xywh2xyxy
-// utils/ops.py:224-240).  One 1024-thread workgroup per image:
+// utils/ops.py:224-240).  nms_best_class_kernel (all CUs) + one 1024-thread workgroup per image:
 //   1. candidates: best class per anchor (first maximum), keep conf > conf_thres, compacted in anchor
-//      order with a block prefix sum;
-//   2. sort by (score desc, anchor asc): bitonic sort of 64-bit keys (LDS up to 8192 candidates,
-//      otherwise in the workspace); truncate to max_nms;
-//   3. class-offset xyxy boxes (cls * max_wh) and areas, in LDS up to 4096 candidates;
-//   4. greedy suppression in sorted order, reproducing the reference's fp32 arithmetic (no FMA
+//      order with a block prefix sum; the class-offset xyxy box (cls * max_wh) and its area are
+//      formed here, where the anchor-ordered loads coalesce;
+//   2. order by (score desc, anchor asc): stable LDS radix sort (4 x 8-bit digits, ballot-matched
+//      ranks) up to 8192 candidates, otherwise a bitonic sort of 64-bit keys in the workspace;
+//      truncate to max_nms;
+//   3. greedy suppression in sorted order, reproducing the reference's fp32 arithmetic (no FMA
 //      contraction in this file) and stopping at max_det.  Fast path (all areas > 0, so no IoU is
-//      NaN and the reference's "no overlap -> keep all" early exit changes nothing): tiles of the
-//      next 64 surviving candidates are resolved sequentially inside one wave (ballots + shuffles),
-//      then every later candidate is tested against the tile's kept boxes in parallel — one
-//      barrier round per tile instead of two per kept box.  Degenerate boxes take the literal
-//      per-box loop (with the early exit) instead.
+//      NaN and the reference's "no overlap -> keep all" early exit changes nothing), by tiles of the
+//      next 64 surviving candidates:
+//        - the 64x64 suppression bit matrix of the tile is built by all 16 waves (one ballot per
+//          row) and resolved in greedy order with 64-bit mask operations;
+//        - later candidates are tested lazily: only those inside a frontier window
+//          [tile end, F) are tested against each tile's kept boxes; a candidate entering the window
+//          is tested once against every box kept so far.  The greedy typically stops (max_det) long
+//          before the end of the sorted list, and nothing past its stop point is ever tested.
+//      Degenerate boxes (or max_det > 1024) take the literal per-box loop with the early exit.
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -20,21 +25,29 @@
 namespace fce {
 
 static constexpr int NMS_THREADS = 1024;
-static constexpr int LDS_SORT_CAP = 8192;
-static constexpr int LDS_BOX_CAP = 4096;
+static constexpr int NWAVES = NMS_THREADS / 64;
+static constexpr int RADIX_CAP = 8192;   // LDS radix sort capacity (16 waves x 512)
 static constexpr int REMOVED_CAP = 32768;
+static constexpr int KEPT_CAP = 1024;    // kept boxes held in LDS by the tiled path
 static constexpr int TILE = 64;
+static constexpr int WIN = NMS_THREADS;  // frontier extension step
+
+// LDS pool (bytes): sort phase  | keysA 32K | keysB 32K | valsA 16K | valsB 16K | wcnt 16K |
+//                   greedy      | removed   | kept box+area | spos (= sorted valsA) |
+static constexpr int POOL = 112 * 1024;
+static constexpr int OFF_KB = 32 * 1024, OFF_VA = 64 * 1024, OFF_VB = 80 * 1024, OFF_WC = 96 * 1024;
+static constexpr int OFF_KBOX = 32 * 1024, OFF_KAREA = 48 * 1024, OFF_KIDX = 52 * 1024;
 
 struct NmsWs {
-  float* aconf;     // per-anchor best score    [A]   (nms_best_class_kernel)
-  int* acls;        // per-anchor best class    [A]
-  int* cidx;        // candidate anchor index   [A]
-  float* cscore;    // candidate score          [A]
-  int* ccls;        // candidate class          [A]
-  uint64_t* keys;   // sort keys                [P2]
-  float4* obox;     // class-offset xyxy        [M]
-  float* area;      //                          [M]
-  int* spos;        // sorted -> candidate pos  [M]
+  float* aconf;    // per-anchor best score    [A]   (nms_best_class_kernel)
+  int* acls;       // per-anchor best class    [A]
+  int* cidx;       // candidate anchor index   [A]
+  float* cscore;   // candidate score          [A]
+  int* ccls;       // candidate class          [A]
+  float4* cbox;    // candidate class-offset xyxy [A]
+  float* carea;    // candidate area           [A]
+  uint64_t* keys;  // global sort keys         [P2]  (> RADIX_CAP candidates)
+  int* spos;       // sorted -> candidate pos  [M]   (> RADIX_CAP candidates)
 };
 
 static int next_pow2(int v) {
@@ -47,7 +60,7 @@ static size_t nms_ws_per_image(int A, int max_nms) {
   const size_t M = std::min(A, max_nms);
   const size_t P2 = next_pow2(std::max(A, 1));
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-  return al(size_t(A) * 4) * 5 + P2 * 8 + M * 16 + al(M * 4) * 2;
+  return al(size_t(A) * 4) * 6 + size_t(A) * 16 + P2 * 8 + al(M * 4);
 }
 
 size_t nms_ws_bytes(int n, int A, int max_nms) { return size_t(n) * nms_ws_per_image(A, max_nms); }
@@ -60,25 +73,20 @@ __device__ __forceinline__ int next_pow2_dev(int v) {
 
 __device__ NmsWs carve(char* p, int A, int max_nms) {
   NmsWs w;
-  const size_t M = min(A, max_nms);
   const int P2 = next_pow2_dev(max(A, 1));
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t a4 = al(size_t(A) * 4);
   w.aconf = reinterpret_cast<float*>(p);
-  p += al(size_t(A) * 4);
-  w.acls = reinterpret_cast<int*>(p);
-  p += al(size_t(A) * 4);
-  w.cidx = reinterpret_cast<int*>(p);
-  p += al(size_t(A) * 4);
-  w.cscore = reinterpret_cast<float*>(p);
-  p += al(size_t(A) * 4);
-  w.ccls = reinterpret_cast<int*>(p);
-  p += al(size_t(A) * 4);
+  w.acls = reinterpret_cast<int*>(p + a4);
+  w.cidx = reinterpret_cast<int*>(p + 2 * a4);
+  w.cscore = reinterpret_cast<float*>(p + 3 * a4);
+  w.ccls = reinterpret_cast<int*>(p + 4 * a4);
+  w.carea = reinterpret_cast<float*>(p + 5 * a4);
+  p += 6 * a4;
+  w.cbox = reinterpret_cast<float4*>(p);
+  p += size_t(A) * 16;
   w.keys = reinterpret_cast<uint64_t*>(p);
   p += size_t(P2) * 8;
-  w.obox = reinterpret_cast<float4*>(p);
-  p += M * 16;
-  w.area = reinterpret_cast<float*>(p);
-  p += al(M * 4);
   w.spos = reinterpret_cast<int*>(p);
   return w;
 }
@@ -92,7 +100,7 @@ __device__ int block_scan(int flag, int* wsum, int* total) {
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
-    for (int i = 0; i < NMS_THREADS / 64; ++i) {
+    for (int i = 0; i < NWAVES; ++i) {
       const int v = wsum[i];
       wsum[i] = acc;
       acc += v;
@@ -121,6 +129,92 @@ __device__ void bitonic_desc(uint64_t* k, int n2) {
   }
 }
 
+// Stable LSD radix sort of RADIX_CAP (key, index) pairs by ascending key, in LDS.  Wave w owns
+// positions [512w, 512w+512) in lane-striped order (item j of lane l = 512w + 64j + l), so the
+// ballot-matched running rank of a digit inside the wave is its stable rank; per-(digit, wave)
+// counts are then scanned digit-major for the global offsets.
+__device__ void radix_sort_lds(uint32_t* kA, uint32_t* kB, uint16_t* vA, uint16_t* vB, int* wcnt, int* wsum) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t* ks = kA;
+  uint32_t* kd = kB;
+  uint16_t* vs = vA;
+  uint16_t* vd = vB;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 8 * pass;
+    for (int e = threadIdx.x; e < NWAVES * 256; e += NMS_THREADS) wcnt[e] = 0;
+    __syncthreads();
+    uint32_t k[8];
+    uint16_t v[8];
+    int d[8], rank[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int idx = 512 * wv + 64 * j + lane;
+      k[j] = ks[idx];
+      v[j] = vs[idx];
+      d[j] = int((k[j] >> shift) & 255u);
+    }
+    int* wc = wcnt + wv * 256;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t peer = ~0ull;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (d[j] >> b) & 1;
+        const uint64_t bal = __ballot(bit);
+        peer &= bit ? bal : ~bal;
+      }
+      const int pre = __popcll(peer & lt);
+      const int base = wc[d[j]];
+      rank[j] = base + pre;
+      __builtin_amdgcn_wave_barrier();
+      if (pre == 0) wc[d[j]] = base + __popcll(peer);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // exclusive scan over e = digit * 16 + wave
+    int c[4], s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x * 4 + i;
+      c[i] = wcnt[(e & 15) * 256 + (e >> 4)];
+      s += c[i];
+    }
+    int inc = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(inc, off);
+      if (lane >= off) inc += t;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int excl = inc - s;
+    for (int i = 0; i < wv; ++i) excl += wsum[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x * 4 + i;
+      wcnt[(e & 15) * 256 + (e >> 4)] = excl;
+      excl += c[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int pos = wc[d[j]] + rank[j];
+      kd[pos] = k[j];
+      vd[pos] = v[j];
+    }
+    __syncthreads();
+    uint32_t* tk = ks;
+    ks = kd;
+    kd = tk;
+    uint16_t* tv = vs;
+    vs = vd;
+    vd = tv;
+  }
+  // 4 passes: the result is back in (kA, vA)
+}
+
 // reference IoU (nms.py:276-291) in fp32, same operation order
 __device__ __forceinline__ float iou_ref(float4 bi, float ai, float4 bj, float aj, float* inter_out) {
   const float ww = fmaxf(fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x), 0.0f);
@@ -128,6 +222,15 @@ __device__ __forceinline__ float iou_ref(float4 bi, float ai, float4 bj, float a
   const float inter = ww * hh;
   *inter_out = inter;
   return inter / ((ai + aj) - inter);
+}
+
+// iou_ref(...) > thr for positive areas: a zero intersection gives IoU 0 (thr >= 0), skip the division
+__device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float aj, float thr) {
+  const float ww = fmaxf(fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x), 0.0f);
+  const float hh = fmaxf(fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y), 0.0f);
+  const float inter = ww * hh;
+  if (inter == 0.0f) return false;
+  return inter / ((ai + aj) - inter) > thr;
 }
 
 // best class per anchor (first maximum, like torch.max): one thread per (image, anchor), all CUs
@@ -166,27 +269,22 @@ __global__ __launch_bounds__(256) void nms_best_class_kernel(const float* pred, 
 __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int nc, int A, float conf_thres,
                                                           float iou_thres, int max_det, int max_nms, float max_wh,
                                                           char* ws, size_t ws_per_image, float* dets, int64_t* keep,
-                                                          int32_t* counts) {
-  __shared__ __attribute__((aligned(16))) uint64_t lkeys[LDS_SORT_CAP];  // sort keys, then float4 boxes
-  __shared__ float larea[LDS_BOX_CAP];
-  __shared__ int lspos[LDS_BOX_CAP];
-  __shared__ uint8_t lremoved[REMOVED_CAP];
-  __shared__ int wsum[NMS_THREADS / 64];
+                                                          int32_t* counts, int stop) {
+  __shared__ __attribute__((aligned(16))) char pool[POOL];
+  __shared__ int wsum[NWAVES];
   __shared__ int tile_idx[TILE];
   __shared__ float4 tile_box[TILE];
   __shared__ float tile_area[TILE];
   __shared__ uint64_t tile_sup[TILE];
-  __shared__ float4 kept_box[TILE];
-  __shared__ float kept_area[TILE];
-  __shared__ int s_total, s_tile_n, s_next, s_nk, s_done, s_kept;
+  __shared__ int s_total, s_tile_n, s_need, s_next, s_nk, s_done, s_kept;
 
   const int n = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* P = pred + int64_t(n) * (4 + nc) * A;
   NmsWs w = carve(ws + size_t(n) * ws_per_image, A, max_nms);
 
-  // ---- 1. candidates in anchor order (best class per anchor from nms_best_class_kernel)
-  int base = 0;
+  // ---- 1. candidates in anchor order (+ their class-offset boxes)
+  int base = 0, degenerate = 0;
   for (int a0 = 0; a0 < A; a0 += NMS_THREADS) {
     const int a = a0 + threadIdx.x;
     float best = -INFINITY;
@@ -198,54 +296,65 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
     const int flag = (a < A) && (best > conf_thres);
     const int pos = block_scan(flag, wsum, &s_total);
     if (flag) {
-      w.cidx[base + pos] = a;
-      w.cscore[base + pos] = best;
-      w.ccls[base + pos] = bj;
+      const int c = base + pos;
+      w.cidx[c] = a;
+      w.cscore[c] = best;
+      w.ccls[c] = bj;
+      const float cx = P[a], cy = P[int64_t(1) * A + a];
+      const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
+      const float off = (float)bj * max_wh;
+      const float bx1 = (cx - hw) + off, by1 = (cy - hh) + off, bx2 = (cx + hw) + off, by2 = (cy + hh) + off;
+      w.cbox[c] = make_float4(bx1, by1, bx2, by2);
+      const float ar = (bx2 - bx1) * (by2 - by1);
+      w.carea[c] = ar;
+      degenerate |= !(ar > 0.0f) || !isfinite(ar);
     }
     base += s_total;
     __syncthreads();
   }
   const int ncand = base;
-
-  // ---- 2. sort (score desc, candidate position asc)
-  const int n2 = next_pow2_dev(max(ncand, 1));
-  uint64_t* keys = n2 <= LDS_SORT_CAP ? lkeys : w.keys;
-  for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-    uint64_t k = 0;
-    if (i < ncand) k = (uint64_t(__float_as_uint(w.cscore[i])) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(i));
-    keys[i] = k;
-  }
-  __syncthreads();
-  if (ncand > 1) bitonic_desc(keys, n2);
-  const int M = min(ncand, max_nms);
-  const bool lds_box = M <= LDS_BOX_CAP;
-  int* spos = lds_box ? lspos : w.spos;
-  float4* obox = lds_box ? reinterpret_cast<float4*>(lkeys) : w.obox;
-  float* area = lds_box ? larea : w.area;
-  for (int i = threadIdx.x; i < M; i += blockDim.x) spos[i] = int(0xFFFFFFFFu - uint32_t(keys[i] & 0xFFFFFFFFull));
-  __syncthreads();  // keys are dead from here (the LDS key space becomes the box array)
-
-  // ---- 3. class-offset boxes
-  int degenerate = 0;
-  for (int i = threadIdx.x; i < M; i += blockDim.x) {
-    const int pos = spos[i];
-    const int a = w.cidx[pos];
-    const float cx = P[a], cy = P[int64_t(1) * A + a];
-    const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
-    const float off = (float)w.ccls[pos] * max_wh;
-    const float bx1 = (cx - hw) + off, by1 = (cy - hh) + off, bx2 = (cx + hw) + off, by2 = (cy + hh) + off;
-    obox[i] = make_float4(bx1, by1, bx2, by2);
-    const float ar = (bx2 - bx1) * (by2 - by1);
-    area[i] = ar;
-    lremoved[i] = 0;
-    degenerate |= !(ar > 0.0f) || !isfinite(ar);
-  }
-  if (threadIdx.x == 0) s_kept = 0;
   degenerate = __syncthreads_or(degenerate);
+  if (stop == 1) return;  // phase timing (FCE_NMS_STOP, diagnostics only)
 
-  auto emit_det = [&](int i, int slot) {
-    const int pos = spos[i];
-    const int a = w.cidx[pos];
+  // ---- 2. order (score desc, candidate position asc)
+  const bool lds_sorted = ncand <= RADIX_CAP;
+  const uint16_t* spos16 = reinterpret_cast<const uint16_t*>(pool + 0);
+  if (lds_sorted) {
+    uint32_t* kA = reinterpret_cast<uint32_t*>(pool);
+    uint16_t* vA = reinterpret_cast<uint16_t*>(pool + OFF_VA);
+    for (int i = threadIdx.x; i < RADIX_CAP; i += NMS_THREADS) {
+      kA[i] = i < ncand ? ~__float_as_uint(w.cscore[i]) : 0xFFFFFFFFu;  // scores > conf >= 0
+      vA[i] = uint16_t(i);
+    }
+    __syncthreads();
+    radix_sort_lds(kA, reinterpret_cast<uint32_t*>(pool + OFF_KB), vA, reinterpret_cast<uint16_t*>(pool + OFF_VB),
+                   reinterpret_cast<int*>(pool + OFF_WC), wsum);
+    spos16 = vA;
+  } else {
+    const int n2 = next_pow2_dev(ncand);
+    for (int i = threadIdx.x; i < n2; i += NMS_THREADS) {
+      uint64_t k = 0;
+      if (i < ncand) k = (uint64_t(__float_as_uint(w.cscore[i])) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(i));
+      w.keys[i] = k;
+    }
+    __syncthreads();
+    bitonic_desc(w.keys, n2);
+    for (int i = threadIdx.x; i < min(ncand, max_nms); i += NMS_THREADS)
+      w.spos[i] = int(0xFFFFFFFFu - uint32_t(w.keys[i] & 0xFFFFFFFFull));
+    __syncthreads();
+  }
+  const int M = min(ncand, max_nms);
+  auto sp = [&](int i) -> int { return lds_sorted ? int(spos16[i]) : w.spos[i]; };
+  uint8_t* lremoved = reinterpret_cast<uint8_t*>(pool);  // sort keys are dead from here
+  float4* kbox = reinterpret_cast<float4*>(pool + OFF_KBOX);
+  float* karea = reinterpret_cast<float*>(pool + OFF_KAREA);
+  int* kidx = reinterpret_cast<int*>(pool + OFF_KIDX);  // kept slot -> candidate (dets written at the end)
+  if (threadIdx.x == 0) s_kept = 0;
+  __syncthreads();
+  if (stop == 2) return;
+
+  auto emit_det = [&](int c, int slot) {
+    const int a = w.cidx[c];
     const float cx = P[a], cy = P[int64_t(1) * A + a];
     const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
     float* d = dets + (int64_t(n) * max_det + slot) * 6;
@@ -253,57 +362,105 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
     d[1] = cy - hh;
     d[2] = cx + hw;
     d[3] = cy + hh;
-    d[4] = w.cscore[pos];
-    d[5] = (float)w.ccls[pos];
+    d[4] = w.cscore[c];
+    d[5] = (float)w.ccls[c];
     keep[int64_t(n) * max_det + slot] = a;
   };
 
-  if (!degenerate) {
-    // ---- 4a. tiled greedy (exact when every area > 0).  Per tile of the next 64 surviving
-    // candidates: (i) wave 0 gathers them; (ii) all 16 waves build the tile's suppression rows
-    // sup[t] = {u > t : IoU(t, u) > thr} with one ballot each; (iii) wave 0 resolves the greedy
-    // order with 64-bit mask operations; (iv) every later candidate is tested against the kept
-    // members in parallel.
-    int cursor = 0;
-    while (true) {
-      if (wv == 0) {
-        int cnt = 0, c = cursor;
-        while (cnt < TILE && c < M) {
-          const int j = c + lane;
-          const bool alive = j < M && !lremoved[j];
-          const uint64_t b = __ballot(alive);
-          const int avail = __popcll(b);
-          const int take = min(avail, TILE - cnt);
-          const int rank = __popcll(b & ((1ull << lane) - 1ull));
-          if (alive && rank < take) tile_idx[cnt + rank] = j;
-          cnt += take;
-          c += 64;
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile_idx writes have landed
-        __builtin_amdgcn_wave_barrier();
-        if (lane < cnt) {
-          const int my = tile_idx[lane];
-          tile_box[lane] = obox[my];
-          tile_area[lane] = area[my];
-        }
-        if (lane == 0) {
-          s_tile_n = cnt;
-          s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : M;  // resume right after the last member
-        }
+  // Lanes' candidates (bj, aj) vs kept boxes [kf, kl): the kept boxes are staged 64 at a time in
+  // lane registers and broadcast with v_readlane, so the inner loop is VALU only (no LDS latency).
+  auto kept_suppress = [&](float4 bj, float aj, bool act, int kf, int kl) -> bool {
+    bool rem = false;
+    for (int c0 = kf; c0 < kl; c0 += 64) {
+      const int m = min(64, kl - c0);
+      float4 kb = make_float4(0.f, 0.f, 0.f, 0.f);
+      float ka = 0.f;
+      if (lane < m) {
+        kb = kbox[c0 + lane];
+        ka = karea[c0 + lane];
       }
-      __syncthreads();
+      auto rl = [](float x, int t) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), t)); };
+      for (int t = 0; t < m; ++t) {
+        const float4 b = make_float4(rl(kb.x, t), rl(kb.y, t), rl(kb.z, t), rl(kb.w, t));
+        const float a = rl(ka, t);
+        if (act && !rem) rem = suppresses(b, a, bj, aj, iou_thres);
+      }
+    }
+    return rem;
+  };
+
+  if (!degenerate && max_det <= KEPT_CAP) {
+    // ---- 3a. tiled greedy with a lazy frontier (exact when every area > 0)
+    int cursor = 0, F = 0;
+    uint64_t tm[6] = {0, 0, 0, 0, 0, 0}, tprev = stop == 9 ? __builtin_amdgcn_s_memtime() : 0;
+    auto tick = [&](int slot) {  // diagnostics (FCE_NMS_STOP=9): barrier-to-barrier segment clocks
+      if (stop == 9) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        tm[slot] += t - tprev;
+        tprev = t;
+      }
+    };
+    while (true) {
+      // select the next <= 64 surviving candidates in [cursor, F), extending F while short
+      while (true) {
+        if (wv == 0) {
+          int cnt = 0;
+          for (int c = cursor; cnt < TILE && c < F; c += 64) {
+            const int j = c + lane;
+            const bool alive = j < F && !lremoved[j];
+            const uint64_t b = __ballot(alive);
+            const int take = min(__popcll(b), TILE - cnt);
+            const int rank = __popcll(b & ((1ull << lane) - 1ull));
+            if (alive && rank < take) tile_idx[cnt + rank] = j;
+            cnt += take;
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile_idx writes have landed
+          __builtin_amdgcn_wave_barrier();
+          const bool need = cnt < TILE && F < M;
+          if (!need && lane < cnt) {
+            const int c = sp(tile_idx[lane]);
+            tile_box[lane] = w.cbox[c];
+            tile_area[lane] = w.carea[c];
+          }
+          if (lane == 0) {
+            s_tile_n = cnt;
+            s_need = need;
+            s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : M;
+          }
+        }
+        __syncthreads();
+        tick(0);
+        if (!s_need) break;
+        // candidates entering the window: test once against every box kept so far
+        const int Fn = min(M, F + WIN), nkept = s_kept;
+        for (int jb = F + wv * 64; jb < Fn; jb += NMS_THREADS) {  // wave-uniform trip count
+          const int j = jb + lane;
+          const bool act = j < Fn;
+          float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+          float aj = 0.f;
+          if (act) {
+            const int c = sp(j);
+            bj = w.cbox[c];
+            aj = w.carea[c];
+          }
+          const bool rem = kept_suppress(bj, aj, act, 0, nkept);
+          if (act) lremoved[j] = rem;
+        }
+        F = Fn;
+        __syncthreads();
+        tick(1);
+      }
       const int cnt = s_tile_n;
       if (cnt == 0) break;
-      for (int t = wv; t < cnt; t += NMS_THREADS / 64) {
+      // suppression rows of the tile: sup[t] = {u > t : IoU(t, u) > thr}
+      for (int t = wv; t < cnt; t += NWAVES) {
         bool sup = false;
-        if (lane > t && lane < cnt) {
-          float inter;
-          sup = iou_ref(tile_box[t], tile_area[t], tile_box[lane], tile_area[lane], &inter) > iou_thres;
-        }
+        if (lane > t && lane < cnt) sup = suppresses(tile_box[t], tile_area[t], tile_box[lane], tile_area[lane], iou_thres);
         const uint64_t b = __ballot(sup);
         if (lane == 0) tile_sup[t] = b;
       }
       __syncthreads();
+      tick(2);
       if (wv == 0) {
         const int kept0 = s_kept;
         const uint64_t mysup = lane < cnt ? tile_sup[lane] : 0ull;
@@ -319,14 +476,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
             done = true;
             break;
           }
-          removed |= uint64_t(__builtin_amdgcn_readlane(sup_lo, t)) |
-                     (uint64_t(__builtin_amdgcn_readlane(sup_hi, t)) << 32);
+          // readlane returns int: go through uint32_t so bit 31 does not sign-extend
+          removed |= uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sup_lo), t))) |
+                     (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sup_hi), t))) << 32);
         }
         if ((keptm >> lane) & 1ull) {
           const int r = __popcll(keptm & ((1ull << lane) - 1ull));
-          kept_box[r] = tile_box[lane];
-          kept_area[r] = tile_area[lane];
-          emit_det(tile_idx[lane], kept0 + r);
+          kbox[kept0 + r] = tile_box[lane];
+          karea[kept0 + r] = tile_area[lane];
+          kidx[kept0 + r] = sp(tile_idx[lane]);
         }
         if (lane == 0) {
           s_nk = nk;
@@ -335,47 +493,59 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
         }
       }
       __syncthreads();
+      tick(3);
       if (s_done) break;
-      // suppress everything after the tile against the tile's kept boxes
-      const int nk = s_nk, start = s_next;
-      for (int j = start + threadIdx.x; j < M; j += blockDim.x) {
-        if (lremoved[j]) continue;
-        const float4 bj = obox[j];
-        const float aj = area[j];
-        for (int k = 0; k < nk; ++k) {
-          float inter;
-          if (iou_ref(kept_box[k], kept_area[k], bj, aj, &inter) > iou_thres) {
-            lremoved[j] = 1;
-            break;
-          }
+      // the rest of the window against the tile's kept boxes
+      const int k0 = s_kept - s_nk, k1 = s_kept, start = s_next;
+      for (int jb = start + wv * 64; jb < F; jb += NMS_THREADS) {  // wave-uniform trip count
+        const int j = jb + lane;
+        const bool act = j < F && !lremoved[j];
+        float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+        float aj = 0.f;
+        if (act) {
+          const int c = sp(j);
+          bj = w.cbox[c];
+          aj = w.carea[c];
         }
+        if (kept_suppress(bj, aj, act, k0, k1)) lremoved[j] = 1;
       }
       cursor = start;
       __syncthreads();
+      tick(4);
+      tm[5] += 1;
     }
+    __syncthreads();
+    for (int slot = threadIdx.x; slot < s_kept; slot += NMS_THREADS) emit_det(kidx[slot], slot);
+    if (stop == 9 && threadIdx.x == 0)
+      for (int i = 0; i < 6; ++i) dets[int64_t(n) * max_det * 6 + i] = float(tm[i]);
   } else {
-    // ---- 4b. literal per-box greedy (TorchNMS.nms with its early exit) for degenerate boxes
+    // ---- 3b. literal per-box greedy (TorchNMS.nms with its early exit) for degenerate boxes
+    for (int i = threadIdx.x; i < M; i += NMS_THREADS) lremoved[i] = 0;
+    __syncthreads();
     int kept = 0;
     for (int i = 0; i < M && kept < max_det; ++i) {
       if (lremoved[i]) continue;
-      if (threadIdx.x == 0) emit_det(i, kept);
+      const int ci = sp(i);
+      if (threadIdx.x == 0) emit_det(ci, kept);
       ++kept;
       if (kept >= max_det) break;
-      const float4 bi = obox[i];
-      const float ai = area[i];
+      const float4 bi = w.cbox[ci];
+      const float ai = w.carea[ci];
       int any = 0;
-      for (int j = i + 1 + threadIdx.x; j < M; j += blockDim.x) {
+      for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
         if (lremoved[j]) continue;
+        const int cj = sp(j);
         float inter;
-        iou_ref(bi, ai, obox[j], area[j], &inter);
+        iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
         any |= inter != 0.0f;
       }
       any = __syncthreads_or(any);
       if (any) {
-        for (int j = i + 1 + threadIdx.x; j < M; j += blockDim.x) {
+        for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
           if (lremoved[j]) continue;
+          const int cj = sp(j);
           float inter;
-          const float iou = iou_ref(bi, ai, obox[j], area[j], &inter);
+          const float iou = iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
           if (!(iou <= iou_thres)) lremoved[j] = 1;
         }
       }
@@ -395,11 +565,13 @@ int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_
   if (n == 0) return FCE_OK;
   const size_t per = nms_ws_per_image(A, max_nms);
   FCE_CHECK(ws && ws_bytes >= per * n, "nms: workspace too small");
+  const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
+  const int stop = stop_env ? atoi(stop_env) : 0;
   if (A > 0)
     hipLaunchKernelGGL(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);
   hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, nc, A, conf, iou, max_det, max_nms, max_wh,
-                     static_cast<char*>(ws), per, dets, keep, counts);
+                     static_cast<char*>(ws), per, dets, keep, counts, stop);
   return launch_status("nms_kernel");
 }
 

@@ -1,0 +1,44 @@
+"""Phase timing of the device NMS on the bench workload (FCE_NMS_STOP=k ends the kernel after phase k)."""
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import fce_pkg  # noqa: E402
+
+fce_pkg.load()
+from fce_yolo_amd.engine import NMS, Engine  # noqa: E402
+from fce_yolo_amd.parser import DetectionModel  # noqa: E402
+from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
+
+dev = torch.device("cuda:0")
+model = DetectionModel("yolo11n-fce.yaml")
+model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
+model.eval().to(dev)
+B = int(os.environ.get("B", 32))
+x = torch.rand(B, 3, 640, 640, generator=torch.Generator().manual_seed(1000)).half().to(dev)
+eng = Engine(model, B, 640, dev)
+pred = eng(x).clone()
+nms = NMS(B, eng.anchors, eng.nc, dev)
+for stop in ("1", "2", "3", "0"):
+    os.environ["FCE_NMS_STOP"] = stop
+    for _ in range(3):
+        nms(pred)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        nms(pred)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"stop={stop}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per call", flush=True)
+print("kept", nms.counts.tolist()[:8])
+os.environ["FCE_NMS_STOP"] = "9"
+nms(pred)
+torch.cuda.synchronize()
+t = nms.dets[:4, 0, :].cpu().tolist()
+print("segment clocks [select, extend, sup, resolve, window, tiles] (s_memtime):")
+for r in t:
+    print("  ", [int(v) for v in r])
