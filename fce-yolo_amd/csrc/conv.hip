@@ -20,8 +20,9 @@ namespace fce {
 
 // ============================================================================ packing (host)
 // nsteps K-steps of 32 (4 chunks of 8 input channels); each cout tile stores nalloc >= nsteps
-// fragments: rounded up to even (the main loop consumes steps in pairs) + 2 zero fragments, so the
-// branch-free prefetch of steps s+2 / s+3 never reads past the image.
+// fragments: rounded up to a multiple of 8 (the main loop consumes steps in groups of its pipeline
+// depth D <= 8) + 8 zero fragments, so the branch-free prefetch D steps ahead never reads past the
+// image.
 struct DenseGeom {
   int cpt, taps, nchunk, nsteps, nalloc, cotiles;
 };
@@ -31,7 +32,7 @@ static DenseGeom dense_geom(const fce_conv_desc& d) {
   g.taps = d.k * d.k;
   g.nchunk = g.taps * g.cpt;
   g.nsteps = (g.nchunk + 3) / 4;
-  g.nalloc = ((g.nsteps + 1) & ~1) + 2;
+  g.nalloc = ((g.nsteps + 7) & ~7) + 8;
   g.cotiles = (d.cout + 15) / 16;
   return g;
 }
@@ -102,8 +103,8 @@ struct ConvArgs {
   int act;
   const float* fw;
   int fn, fi;
-  int cpt, nchunk, nsteps;  // nsteps: even (loop runs in pairs)
-  int nalloc;               // fragments stored per cout tile (nsteps + 2 zero pad)
+  int cpt, nchunk, nsteps;  // nsteps: multiple of the kernel's pipeline depth (set at launch)
+  int nalloc;               // fragments stored per cout tile (see dense_geom)
   unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
   int vec_ok;
   // fused Detect tail (OUT_DFL / OUT_CLS): pred (N, 4+nc, A) fp32
@@ -114,8 +115,17 @@ struct ConvArgs {
 
 enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3, OUT_DFL = 4, OUT_CLS = 5 };
 
+// Software-pipeline depth: K-steps of fragments in flight per wave.  Small register tiles have little
+// MFMA work per step to cover a load's latency, so they keep more steps in flight (the summation
+// order over K is the same for every depth).
+template <int RC, int RP>
+struct ConvDepth {
+  static constexpr int D = RC * RP == 1 ? 8 : RC * RP == 2 ? 4 : 2;
+};
+
 template <int KS, int RC, int RP, int OUT, bool FAST>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+  constexpr int D = ConvDepth<RC, RP>::D;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int col = lane & 15;
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 
   // Branch-free K loop: an out-of-image tap or padded K chunk loads a 16-byte zero line (address
   // select, never a value mask), so no load is conditional and hipcc places counted vmcnt waits;
-  // two K-steps of fragments stay in flight (ring set 0 / set 1, unrolled: static indices).
+  // D K-steps of fragments stay in flight (a ring of D register sets, unrolled: static indices).
   // FAST (cin % 32 == 0): a K-step is 32 channels of ONE tap, so the (tap, step-in-tap) cursor is
   // wave-uniform (scalar).  Otherwise each lane decodes its chunk c = 4s+grp with a magic divide.
   const h8* wfrag[RC];
@@ -202,24 +212,23 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int r = 0; r < RC; ++r) w[r] = wfrag[r][s * 64];
   };
-  h8 b0[RP], b1[RP], a0[RC], a1[RC];
-  load_b(0, b0);
-  load_a(0, a0);
-  load_b(1, b1);
-  load_a(1, a1);
-  for (int s = 0; s < a.nsteps; s += 2) {  // nsteps rounded up to even: padded steps are zero
+  h8 bq[D][RP], aq[D][RC];
 #pragma unroll
-    for (int r = 0; r < RC; ++r)
+  for (int d = 0; d < D; ++d) {
+    load_b(d, bq[d]);
+    load_a(d, aq[d]);
+  }
+  for (int s = 0; s < a.nsteps; s += D) {  // nsteps rounded up to a multiple of D: padded steps are zero
 #pragma unroll
-      for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[r], b0[p], acc[r][p], 0, 0, 0);
-    load_b(s + 2, b0);
-    load_a(s + 2, a0);
+    for (int d = 0; d < D; ++d) {
 #pragma unroll
-    for (int r = 0; r < RC; ++r)
+      for (int r = 0; r < RC; ++r)
 #pragma unroll
-      for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[r], b1[p], acc[r][p], 0, 0, 0);
-    load_b(s + 3, b1);
-    load_a(s + 3, a1);
+        for (int p = 0; p < RP; ++p)
+          acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aq[d][r], bq[d][p], acc[r][p], 0, 0, 0);
+      load_b(s + D + d, bq[d]);
+      load_a(s + D + d, aq[d]);
+    }
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -656,16 +665,23 @@ static void launch_dense(const ConvArgs& a, int out_kind, bool fast, dim3 grid, 
 #undef CONV_L
 }
 
+template <int KS, int RC, int RP>
+static void launch_dense_d(ConvArgs a, int out_kind, bool fast, dim3 grid, hipStream_t s) {
+  constexpr int D = ConvDepth<RC, RP>::D;
+  a.nsteps = (a.nsteps + D - 1) / D * D;  // the prefetch reads up to step nsteps + D - 1 < nalloc
+  launch_dense<KS, RC, RP>(a, out_kind, fast, grid, s);
+}
+
 template <int KS, int RP>
 static void launch_dense_rp(const ConvArgs& a, int out_kind, bool fast, int rc, hipStream_t s) {
   const int cotiles = (a.cout + 15) / 16;
   dim3 grid((a.P + 64 * RP - 1) / (64 * RP), (cotiles + rc - 1) / rc);
   if (rc == 1)
-    launch_dense<KS, 1, RP>(a, out_kind, fast, grid, s);
+    launch_dense_d<KS, 1, RP>(a, out_kind, fast, grid, s);
   else if (rc == 2)
-    launch_dense<KS, 2, RP>(a, out_kind, fast, grid, s);
+    launch_dense_d<KS, 2, RP>(a, out_kind, fast, grid, s);
   else
-    launch_dense<KS, 4, RP>(a, out_kind, fast, grid, s);
+    launch_dense_d<KS, 4, RP>(a, out_kind, fast, grid, s);
 }
 
 // Tile choice: a wave owns (16*RC couts) x (16*RP pixels).  Big tiles reuse each loaded fragment
@@ -830,10 +846,10 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.fi = d.fusion_i;
   a.cpt = g.cpt;
   a.nchunk = g.nchunk;
-  a.nsteps = (g.nsteps + 1) & ~1;
+  a.nsteps = g.nsteps;  // rounded up to the pipeline depth at launch (launch_dense_d)
   a.nalloc = g.nalloc;
   a.cmagic = g.cpt > 1 ? unsigned(0xFFFFFFFFull / unsigned(g.cpt) + 1ull) : 0u;
-  FCE_CHECK(g.nalloc >= a.nsteps + 2 && g.nchunk + 16 < 65536, "conv: K too large for the chunk cursor");
+  FCE_CHECK(g.nalloc >= ((g.nsteps + 7) & ~7) + 8 && g.nchunk + 64 < 65536, "conv: K too large for the chunk cursor");
   a.vec_ok = (y.cstride % 4 == 0 && y.coff % 4 == 0 && (!res || (res->cstride % 4 == 0 && res->coff % 4 == 0))) ? 1 : 0;
   if (out_kind == OUT_WSTORE || out_kind == OUT_ACCUM) FCE_CHECK(d.fusion_w && d.fusion_n > d.fusion_i, "conv: fusion weights");
   a.pred = det ? det->pred : nullptr;

@@ -98,7 +98,7 @@ def _pack_ref(w, cin, cout, k):
     cpt, taps = cin // 8, k * k
     nchunk = taps * cpt
     nsteps = (nchunk + 3) // 4
-    nalloc = ((nsteps + 1) & ~1) + 2  # even + 2 zero fragments for the branch-free prefetch
+    nalloc = ((nsteps + 7) & ~7) + 8  # multiple of 8 + 8 zero fragments for the depth-D prefetch
     cot = (cout + 15) // 16
     out = np.zeros((cot, nalloc, 64, 8), np.float16)
     for ct in range(cot):
