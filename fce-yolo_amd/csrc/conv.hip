@@ -103,7 +103,7 @@ struct ConvArgs {
   int act;
   const float* fw;
   int fn, fi;
-  int cpt, nchunk, nsteps;  // nsteps: multiple of the kernel's pipeline depth (set at launch)
+  int cpt, nchunk, nsteps;  // K-steps of 32
   int nalloc;               // fragments stored per cout tile (see dense_geom)
   unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
   int vec_ok;
@@ -218,7 +218,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     load_b(d, bq[d]);
     load_a(d, aq[d]);
   }
-  for (int s = 0; s < a.nsteps; s += D) {  // nsteps rounded up to a multiple of D: padded steps are zero
+  const int full = a.nsteps - a.nsteps % D;
+  for (int s = 0; s < full; s += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
 #pragma unroll
@@ -226,8 +227,19 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
         for (int p = 0; p < RP; ++p)
           acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aq[d][r], bq[d][p], acc[r][p], 0, 0, 0);
-      load_b(s + D + d, bq[d]);
+      load_b(s + D + d, bq[d]);  // reads at most step nsteps + D - 1 < nalloc (zero padded)
       load_a(s + D + d, aq[d]);
+    }
+  }
+  // tail: steps full .. nsteps-1 already sit in ring slots 0 .. rem-1
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (d < a.nsteps - full) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+#pragma unroll
+        for (int p = 0; p < RP; ++p)
+          acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aq[d][r], bq[d][p], acc[r][p], 0, 0, 0);
     }
   }
 
@@ -665,23 +677,16 @@ static void launch_dense(const ConvArgs& a, int out_kind, bool fast, dim3 grid, 
 #undef CONV_L
 }
 
-template <int KS, int RC, int RP>
-static void launch_dense_d(ConvArgs a, int out_kind, bool fast, dim3 grid, hipStream_t s) {
-  constexpr int D = ConvDepth<RC, RP>::D;
-  a.nsteps = (a.nsteps + D - 1) / D * D;  // the prefetch reads up to step nsteps + D - 1 < nalloc
-  launch_dense<KS, RC, RP>(a, out_kind, fast, grid, s);
-}
-
 template <int KS, int RP>
 static void launch_dense_rp(const ConvArgs& a, int out_kind, bool fast, int rc, hipStream_t s) {
   const int cotiles = (a.cout + 15) / 16;
   dim3 grid((a.P + 64 * RP - 1) / (64 * RP), (cotiles + rc - 1) / rc);
   if (rc == 1)
-    launch_dense_d<KS, 1, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 1, RP>(a, out_kind, fast, grid, s);
   else if (rc == 2)
-    launch_dense_d<KS, 2, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 2, RP>(a, out_kind, fast, grid, s);
   else
-    launch_dense_d<KS, 4, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 4, RP>(a, out_kind, fast, grid, s);
 }
 
 // Tile choice: a wave owns (16*RC couts) x (16*RP pixels).  Big tiles reuse each loaded fragment
@@ -846,7 +851,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.fi = d.fusion_i;
   a.cpt = g.cpt;
   a.nchunk = g.nchunk;
-  a.nsteps = g.nsteps;  // rounded up to the pipeline depth at launch (launch_dense_d)
+  a.nsteps = g.nsteps;
   a.nalloc = g.nalloc;
   a.cmagic = g.cpt > 1 ? unsigned(0xFFFFFFFFull / unsigned(g.cpt) + 1ull) : 0u;
   FCE_CHECK(g.nalloc >= ((g.nsteps + 7) & ~7) + 8 && g.nchunk + 64 < 65536, "conv: K too large for the chunk cursor");
