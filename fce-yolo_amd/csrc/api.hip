@@ -18,9 +18,10 @@ namespace fce {
 size_t conv_weight_bytes(const fce_conv_desc& d);
 int conv_pack(const fce_conv_desc& d, const float* w, void* out);
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s);
+           const fce_tensor& y, hipStream_t s, int tile = -1);
 int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
-                  const fce_detect_epi& e, hipStream_t s);
+                  const fce_detect_epi& e, hipStream_t s, int tile = -1);
+int conv_tile_candidates(const fce_conv_desc& d, int det_box, int* out, int cap);
 int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
                   hipStream_t s);
 int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor& y,
@@ -175,6 +176,7 @@ struct OpDesc {
   float strides[4] = {0, 0, 0, 0};
   int reg_max = 16;
   int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT
+  int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
 };
 
 }  // namespace
@@ -253,7 +255,7 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
         r = net->view(op.res, op.res_coff, op.conv.cout);
         rp = &r;
       }
-      return conv2d(op.conv, x, op.w, op.b, rp, y, s);
+      return conv2d(op.conv, x, op.w, op.b, rp, y, s, op.tile);
     }
     case OP_MAXPOOL: {
       const int c = op.in_c;
@@ -277,7 +279,7 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
     }
     case OP_CONV_DETECT: {
       fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, op.part, op.strides[0]};
-      return conv2d_detect(op.conv, x, op.w, op.b, e, s);
+      return conv2d_detect(op.conv, x, op.w, op.b, e, s, op.tile);
     }
     case OP_DETECT: {
       fce_tensor bx[4], cl[4];
@@ -526,6 +528,61 @@ int fce_net_add_conv_detect(fce_net* net, const fce_conv_desc* d, int in, int in
   return FCE_OK;
 }
 
+// Plan-time tile autotuning: every dense conv is timed (on the planned shapes, arena contents) with
+// each candidate register tile and keeps the fastest.  Small maps favour fewer, fuller tiles (L2
+// traffic) over occupancy in ways a closed-form rule does not capture reliably.
+static int autotune(fce_net* net) {
+  hipStream_t ts = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float* pred = nullptr;
+  int st = FCE_OK;
+  int nc = 0;
+  for (const OpDesc& op : net->ops)
+    if (op.kind == OP_CONV_DETECT) nc = std::max(nc, op.nc);
+  auto cleanup = [&]() {
+    if (pred) (void)hipFree(pred);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (ts) (void)hipStreamDestroy(ts);
+  };
+  if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess ||
+      (nc > 0 && hipMalloc(reinterpret_cast<void**>(&pred), size_t(net->batch) * (4 + nc) * std::max(net->anchors, 1) *
+                                                                 sizeof(float)) != hipSuccess)) {
+    cleanup();
+    return fail(FCE_ERR_HIP, "fce_net_plan: autotune setup failed");
+  }
+  fce_tensor none{};
+  for (OpDesc& op : net->ops) {
+    if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
+    int cand[16];
+    const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0, cand, 16);
+    if (nc_ <= 1) continue;
+    float best_ms = 1e30f;
+    int best = -1;
+    for (int i = 0; i < nc_ && st == FCE_OK; ++i) {
+      op.tile = cand[i];
+      for (int r = 0; r < 2 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
+      if (st) break;
+      (void)hipEventRecord(e0, ts);
+      for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
+      (void)hipEventRecord(e1, ts);
+      if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (st == FCE_OK && ms < best_ms) {
+        best_ms = ms;
+        best = cand[i];
+      }
+    }
+    op.tile = best;
+    if (st) break;
+  }
+  if (hipStreamSynchronize(ts) != hipSuccess && st == FCE_OK) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune failed");
+  cleanup();
+  return st;
+}
+
 int fce_net_plan(fce_net* net, int batch, int h, int w) {
   FCE_CHECK(net && batch > 0 && h > 0 && w > 0, "fce_net_plan: bad argument");
   FCE_CHECK(h % 32 == 0 && w % 32 == 0, "fce_net_plan: H and W must be multiples of 32 (max stride)");
@@ -568,6 +625,8 @@ int fce_net_plan(fce_net* net, int batch, int h, int w) {
     FCE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&net->arena), std::max<size_t>(off, 256)));
     FCE_HIP_CHECK(hipMalloc(&net->ws, ws));
     FCE_HIP_CHECK(hipMemset(net->arena, 0, std::max<size_t>(off, 256)));
+    const char* at = getenv("FCE_AUTOTUNE");
+    if (!at || atoi(at) != 0) return autotune(net);
     return FCE_OK;
   })
 }

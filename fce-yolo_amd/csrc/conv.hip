@@ -208,9 +208,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
       b[p] = *src;
     }
   };
-  auto load_a = [&](int s, h8 (&w)[RC]) {
+  auto load_a = [&](int s, h8 (&w)[RC]) {  // past the last step: one broadcast zero line, not a 1 KiB fragment
+    const bool in = s < a.nsteps;
 #pragma unroll
-    for (int r = 0; r < RC; ++r) w[r] = wfrag[r][s * 64];
+    for (int r = 0; r < RC; ++r) w[r] = *(in ? wfrag[r] + s * 64 : zline);
   };
   h8 bq[D][RP], aq[D][RC];
 #pragma unroll
@@ -720,8 +721,23 @@ static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, 
     launch_dense_rp<KS, 4>(a, out_kind, fast, rc, s);
 }
 
+// Register tiles a dense conv may run with, encoded rc | rp << 4 (the executor times them at plan
+// time and keeps the fastest; the tile never changes the K summation order, so results are bitwise
+// the same for every choice).  Returns the count; 0 for stem / depthwise convs.
+int conv_tile_candidates(const fce_conv_desc& d, int det_box, int* out, int cap) {
+  if (is_stem(d) || is_dw(d)) return 0;
+  const int cotiles = (d.cout + 15) / 16;
+  int n = 0;
+  for (int rc : {1, 2, 4}) {
+    if (det_box ? rc != 4 : (rc > 1 && (rc >> 1) >= cotiles)) continue;
+    for (int rp : {1, 2, 4})
+      if (n < cap) out[n++] = rc | (rp << 4);
+  }
+  return n;
+}
+
 int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-                const fce_tensor& y, const fce_detect_epi* det, hipStream_t s) {
+                const fce_tensor& y, const fce_detect_epi* det, hipStream_t s, int tile) {
   FCE_CHECK(d.k == 1 || d.k == 3 || (is_stem(d) && d.k <= 7), "conv: kernel size must be 1 or 3");
   FCE_CHECK(d.stride >= 1 && d.stride <= 2, "conv: stride must be 1 or 2");
   FCE_CHECK(x.n == y.n && x.c == d.cin && y.c == d.cout, "conv: channel/batch mismatch");
@@ -865,7 +881,13 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_w = Wo;
   a.det_stride = det ? det->stride : 0.f;
   int rc, rp;
-  pick_tile(a.P, g.cotiles, out_kind == OUT_DFL, &rc, &rp);
+  if (tile >= 0) {
+    rc = tile & 15;
+    rp = tile >> 4;
+    FCE_CHECK((rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4), "conv: bad tile hint");
+  } else {
+    pick_tile(a.P, g.cotiles, out_kind == OUT_DFL, &rc, &rp);
+  }
   if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
   if (d.k == 3) FCE_CHECK(d.up == 0 && out_kind == OUT_F16, "conv 3x3: plain fp16 store, no fused upsampling");
   const bool fast = d.cin % 32 == 0;
@@ -877,15 +899,15 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
 }
 
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s) {
-  return conv2d_impl(d, x, w, bias, res, y, nullptr, s);
+           const fce_tensor& y, hipStream_t s, int tile) {
+  return conv2d_impl(d, x, w, bias, res, y, nullptr, s, tile);
 }
 
 int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
-                  const fce_detect_epi& e, hipStream_t s) {
+                  const fce_detect_epi& e, hipStream_t s, int tile) {
   // the output view only carries the spatial geometry; results go to e.pred
   fce_tensor y{nullptr, FCE_F32, FCE_NHWC, x.n, d.cout, x.h, x.w, d.cout, 0};
-  return conv2d_impl(d, x, w, bias, nullptr, y, &e, s);
+  return conv2d_impl(d, x, w, bias, nullptr, y, &e, s, tile);
 }
 
 }  // namespace fce

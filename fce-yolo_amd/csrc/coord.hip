@@ -16,7 +16,7 @@
 namespace fce {
 
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s);
+           const fce_tensor& y, hipStream_t s, int tile = -1);
 
 enum { ACT_NONE_ = 0, ACT_SILU_ = 1, ACT_SIGMOID_ = 2 };
 

@@ -151,3 +151,16 @@ def test_fold_bn_matches_reference_fuse():
     w, b = M.fold_bn(conv.conv, conv.bn)
     f = O.fuse_state_dict({"m." + k: v for k, v in conv.state_dict().items()})
     assert torch.equal(w, f["m.conv.weight"]) and torch.allclose(b, f["m.conv.bias"], atol=1e-7)
+
+
+def test_library_has_no_undefined_internal_symbols():
+    """Every fce:: function the translation units call is defined (a signature drift between a
+    declaration and its definition links fine into a .so and only fails at load on the GPU box)."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("nm"):
+        pytest.skip("nm not available")
+    out = subprocess.run(["nm", "-uC", str(N.LIB_PATH)], capture_output=True, text=True, check=True).stdout
+    bad = [l for l in out.splitlines() if "fce::" in l]
+    assert not bad, bad
