@@ -557,18 +557,49 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 // of one row.  Their receptive columns are the aligned run x[2*PX*q .. 2*PX*q + 2PX-1] plus the
 // element before it, so each (ci, ky) costs one vector load + one scalar load instead of 3*PX.
 // Weights [ci][ky][kx][co] broadcast from LDS; same per-pixel summation order as stem_kernel.
+// NE consecutive input elements held as raw 32-bit words (one aligned vector load)
 template <typename T, int NE>
-__device__ __forceinline__ void load_run(const T* p, float* out) {
-  T tmp[NE];
-  __builtin_memcpy(tmp, __builtin_assume_aligned(p, sizeof(T) * NE), sizeof(T) * NE);
+struct RawRun {
+  static constexpr int NW = (int(sizeof(T)) * NE + 3) / 4;
+  uint32_t w[NW];
+  __device__ __forceinline__ void load(const T* p) {
+    if constexpr (NW == 8) {
+      const uint4 lo = reinterpret_cast<const uint4*>(p)[0], hi = reinterpret_cast<const uint4*>(p)[1];
+      w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w; w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+    } else if constexpr (NW == 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(p);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if constexpr (NW == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      w[0] = v.x; w[1] = v.y;
+    } else {
+      static_assert(NW == 1, "run size");
+      w[0] = *reinterpret_cast<const uint32_t*>(p);
+    }
+  }
+  __device__ __forceinline__ void zero() {
 #pragma unroll
-  for (int e = 0; e < NE; ++e) out[e] = ld_in<T>(tmp, e);
-}
+    for (int i = 0; i < NW; ++i) w[i] = 0u;
+  }
+  __device__ __forceinline__ float get(int e) const {
+    if constexpr (sizeof(T) == 4) {
+      return __uint_as_float(w[e]);
+    } else if constexpr (sizeof(T) == 2) {
+      const unsigned short h = (unsigned short)(w[e >> 1] >> ((e & 1) * 16));
+      return (float)__ushort_as_half(h);
+    } else {
+      return (float)((w[e >> 2] >> ((e & 3) * 8)) & 255u) * (1.0f / 255.0f);
+    }
+  }
+};
 
-template <int COUT, int PX, typename T>
+template <int COUT, int PX, typename T, bool DB>
 __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
+  // RGB only (CIN = 3): all 9 (channel, row) runs are loaded before any arithmetic, so a wave waits
+  // on HBM once instead of nine times.
+  constexpr int CIN = 3, NE = 2 * PX;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nw = a.C * 9 * COUT;
+  const int nw = CIN * 9 * COUT;
   for (int i = threadIdx.x; i < nw; i += blockDim.x) {
     const int co = i % COUT, r = i / COUT;
     smem[i] = co < a.cout ? a.w[r * a.cout + co] : 0.f;
@@ -580,27 +611,43 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
   if (row >= a.N * a.Ho) return;
   const int n = row / a.Ho, oy = row - n * a.Ho;
   const int ix0 = 2 * PX * q;
+  const bool interior = ix0 + NE <= a.W;
   const T* x = static_cast<const T*>(a.x);
+  // channel ci+1's three row runs are in flight while channel ci computes (double buffer; the
+  // channel loop stays rolled so the 27 x COUT weights are re-read from LDS, not held in registers)
+  RawRun<T, NE> cur[3], nxt[3];
+  float cpre[3], npre[3];
+  auto load_ci = [&](int ci, RawRun<T, NE> (&r)[3], float (&p)[3]) {
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = 2 * oy - 1 + ky;
+      const bool rin = iy >= 0 && iy < a.H;
+      const T* rp = x + ((int64_t(n) * CIN + ci) * a.H + (rin ? iy : 0)) * a.W;
+      p[ky] = (rin && ix0 > 0) ? ld_in<T>(rp, ix0 - 1) : 0.f;
+      if (rin && interior)
+        r[ky].load(rp + ix0);
+      else  // image edge rows / partial runs (the dispatcher only launches this kernel for W % 2PX == 0)
+        r[ky].zero();
+    }
+  };
   float acc[PX][COUT];
 #pragma unroll
   for (int j = 0; j < PX; ++j)
 #pragma unroll
     for (int co = 0; co < COUT; ++co) acc[j][co] = 0.f;
-  for (int ci = 0; ci < a.C; ++ci) {
-    const T* plane = x + (int64_t(n) * a.C + ci) * a.H * a.W;
+  if (DB) load_ci(0, cur, cpre);
+#pragma unroll 1
+  for (int ci = 0; ci < CIN; ++ci) {
+    if (!DB)
+      load_ci(ci, cur, cpre);
+    else if (ci + 1 < CIN)
+      load_ci(ci + 1, nxt, npre);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const int iy = 2 * oy - 1 + ky;
-      if (iy < 0 || iy >= a.H) continue;
-      const T* rp = plane + int64_t(iy) * a.W;
-      float v[2 * PX + 1];
-      v[0] = ix0 > 0 ? ld_in<T>(rp, ix0 - 1) : 0.f;
-      if (ix0 + 2 * PX <= a.W) {
-        load_run<T, 2 * PX>(rp + ix0, v + 1);
-      } else {
+      float v[NE + 1];
+      v[0] = cpre[ky];
 #pragma unroll
-        for (int e = 0; e < 2 * PX; ++e) v[1 + e] = ix0 + e < a.W ? ld_in<T>(rp, ix0 + e) : 0.f;
-      }
+      for (int e = 0; e < NE; ++e) v[1 + e] = cur[ky].get(e);
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const float* wt = smem + ((ci * 3 + ky) * 3 + kx) * COUT;
@@ -616,6 +663,13 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
             acc[j][co + 3] += xv * w4[3];
           }
         }
+      }
+    }
+    if (DB) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        cur[ky] = nxt[ky];
+        cpre[ky] = npre[ky];
       }
     }
   }
@@ -759,12 +813,24 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     int coutT = d.cout <= 16 ? 16 : d.cout <= 32 ? 32 : d.cout <= 64 ? 64 : d.cout <= 96 ? 96 : 0;
     FCE_CHECK(coutT > 0, "stem conv: cout > 96 unsupported");
     const size_t shm = size_t(x.c) * d.k * d.k * coutT * sizeof(float);
-    const int PX = coutT <= 16 ? 4 : coutT <= 32 ? 2 : 1;
-    if (d.k == 3 && d.stride == 2 && x.w % (2 * PX) == 0) {
+    int PX = coutT <= 16 ? 4 : coutT <= 32 ? 2 : 1, DB = 0;
+    if (const char* e = getenv("FCE_STEM")) {  // diagnostics: "px,db"
+      PX = atoi(e);
+      const char* c = strchr(e, ',');
+      DB = c ? atoi(c + 1) : 0;
+      if (PX != 1 && PX != 2 && PX != 4) PX = 1;
+    }
+    if (d.k == 3 && d.stride == 2 && x.c == 3 && x.w % (2 * PX) == 0) {
       const int64_t threads = int64_t(x.n) * Ho * ((Wo + PX - 1) / PX);
       FCE_CHECK(threads < (int64_t(1) << 31), "stem conv: input too large");
       const dim3 grid(unsigned((threads + 255) / 256));
-#define STEM2_LAUNCH(CT, P, T) hipLaunchKernelGGL((stem_s2_kernel<CT, P, T>), grid, dim3(256), shm, s, a)
+#define STEM2_LAUNCH(CT, P, T)                                                              \
+  do {                                                                                       \
+    if (DB)                                                                                  \
+      hipLaunchKernelGGL((stem_s2_kernel<CT, P, T, true>), grid, dim3(256), shm, s, a);      \
+    else                                                                                     \
+      hipLaunchKernelGGL((stem_s2_kernel<CT, P, T, false>), grid, dim3(256), shm, s, a);     \
+  } while (0)
 #define STEM2_DT(CT, P)                  \
   do {                                   \
     if (x.dtype == FCE_F16)              \
@@ -774,14 +840,23 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     else                                 \
       STEM2_LAUNCH(CT, P, uint8_t);      \
   } while (0)
-      if (coutT == 16)
-        STEM2_DT(16, 4);
-      else if (coutT == 32)
-        STEM2_DT(32, 2);
-      else if (coutT == 64)
+      if (coutT == 16) {
+        if (PX == 4)
+          STEM2_DT(16, 4);
+        else if (PX == 2)
+          STEM2_DT(16, 2);
+        else
+          STEM2_DT(16, 1);
+      } else if (coutT == 32) {
+        if (PX == 1)
+          STEM2_DT(32, 1);
+        else
+          STEM2_DT(32, 2);
+      } else if (coutT == 64) {
         STEM2_DT(64, 1);
-      else
+      } else {
         STEM2_DT(96, 1);
+      }
 #undef STEM2_DT
 #undef STEM2_LAUNCH
       return launch_status("stem_s2_kernel");
