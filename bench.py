@@ -37,6 +37,28 @@ from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFS = 2500.0  # dense fp16 MFMA (no sparsity)
 RIDGE = MFMA_F16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+PMC_TRAFFIC = Path(__file__).resolve().parent / "profiles" / "pmc_traffic.json"
+
+
+def _pmc_marker(dev):
+    """One 1-element fce_copy dispatch (copy_kernel is not used by the forward) marking where the
+    eager per-op profile pass starts in a rocprofv3 --pmc trace."""
+    import ctypes as C
+
+    from fce_yolo_amd import _native as N
+
+    t = torch.zeros(1, 1, 1, 1, device=dev, dtype=torch.float16)
+    d = N.Tensor(t.data_ptr(), N.F16, N.NCHW, 1, 1, 1, 1, 1, 0)
+    N.call("fce_copy", C.byref(d), C.byref(d), torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _pmc_traffic(family):
+    """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 correction; scripts/gpu_pmc.sh), or None."""
+    try:
+        return float(json.loads(PMC_TRAFFIC.read_text())["families"][family]["hbm_bytes"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
 GFLOP_PER_IMG = {"yolo11n-fce": 6.338, "yolo11s-bifpn": 21.695, "yolo11m-fce": 263.13, "yolo11l-fce": 84.50}
 
 
@@ -142,6 +164,7 @@ def main():
     fwd_ms = (time.perf_counter() - t1) / a.steps * 1e3
 
     # per-op HIP-event profile (eager, same kernels) -> dominant kernel family roofline
+    _pmc_marker(dev)  # delimits the per-op profile pass for scripts/pmc_summary.py
     prof = eng.profile(x)
     fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0])
     for name, nbytes, flops, ms in prof:
@@ -160,7 +183,9 @@ def main():
         ach = dbytes / dn / (dms / dn * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    roof["traffic"] = None
+    tr = _pmc_traffic(dname)
+    roof["traffic"] = None if tr is None else round(tr / 1e6, 3)
+    roof["traffic_unit"] = "MB/launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_traffic.json)"
     roof["kernel"] = dname
     roof["launches_per_step"] = dn
     roof["kernel_ms_per_step"] = round(dms, 4)

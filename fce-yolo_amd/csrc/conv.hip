@@ -593,11 +593,12 @@ struct RawRun {
   }
 };
 
-template <int COUT, int PX, typename T, bool DB>
+template <int COUT, int PX, typename T>
 __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
-  // RGB only (CIN = 3): all 9 (channel, row) runs are loaded before any arithmetic, so a wave waits
-  // on HBM once instead of nine times.
-  constexpr int CIN = 3, NE = 2 * PX;
+  // RGB input (CIN = 3).  Output: when the view is a dense [pixel][COUT] buffer the block stages its
+  // results in LDS and each store instruction writes 64 x 16 contiguous bytes (direct per-thread
+  // stores at a 32*PX-byte lane stride reach HBM as partial lines: 2.4x the output bytes measured).
+  constexpr int CIN = 3, NE = 2 * PX, CPT = PX * COUT / 8;  // 16-byte chunks per thread
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nw = CIN * 9 * COUT;
   for (int i = threadIdx.x; i < nw; i += blockDim.x) {
@@ -606,48 +607,40 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
   }
   __syncthreads();
   const int Q = (a.Wo + PX - 1) / PX;
+  const int nthreads = a.N * a.Ho * Q;
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  const int row = idx / Q, q = idx - row * Q;
-  if (row >= a.N * a.Ho) return;
+  const bool valid = idx < nthreads;
+  const int row = valid ? idx / Q : 0, q = valid ? idx - row * Q : 0;
   const int n = row / a.Ho, oy = row - n * a.Ho;
   const int ix0 = 2 * PX * q;
   const bool interior = ix0 + NE <= a.W;
   const T* x = static_cast<const T*>(a.x);
-  // channel ci+1's three row runs are in flight while channel ci computes (double buffer; the
-  // channel loop stays rolled so the 27 x COUT weights are re-read from LDS, not held in registers)
-  RawRun<T, NE> cur[3], nxt[3];
-  float cpre[3], npre[3];
-  auto load_ci = [&](int ci, RawRun<T, NE> (&r)[3], float (&p)[3]) {
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int iy = 2 * oy - 1 + ky;
-      const bool rin = iy >= 0 && iy < a.H;
-      const T* rp = x + ((int64_t(n) * CIN + ci) * a.H + (rin ? iy : 0)) * a.W;
-      p[ky] = (rin && ix0 > 0) ? ld_in<T>(rp, ix0 - 1) : 0.f;
-      if (rin && interior)
-        r[ky].load(rp + ix0);
-      else  // image edge rows / partial runs (the dispatcher only launches this kernel for W % 2PX == 0)
-        r[ky].zero();
-    }
-  };
   float acc[PX][COUT];
 #pragma unroll
   for (int j = 0; j < PX; ++j)
 #pragma unroll
     for (int co = 0; co < COUT; ++co) acc[j][co] = 0.f;
-  if (DB) load_ci(0, cur, cpre);
 #pragma unroll 1
   for (int ci = 0; ci < CIN; ++ci) {
-    if (!DB)
-      load_ci(ci, cur, cpre);
-    else if (ci + 1 < CIN)
-      load_ci(ci + 1, nxt, npre);
+    RawRun<T, NE> run[3];
+    float pre[3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {  // the three row loads of a channel are issued together
+      const int iy = 2 * oy - 1 + ky;
+      const bool rin = valid && iy >= 0 && iy < a.H;
+      const T* rp = x + ((int64_t(n) * CIN + ci) * a.H + (rin ? iy : 0)) * a.W;
+      pre[ky] = (rin && ix0 > 0) ? ld_in<T>(rp, ix0 - 1) : 0.f;
+      if (rin && interior)
+        run[ky].load(rp + ix0);
+      else  // rows outside the image (the dispatcher only launches this kernel for W % 2PX == 0)
+        run[ky].zero();
+    }
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
       float v[NE + 1];
-      v[0] = cpre[ky];
+      v[0] = pre[ky];
 #pragma unroll
-      for (int e = 0; e < NE; ++e) v[1 + e] = cur[ky].get(e);
+      for (int e = 0; e < NE; ++e) v[1 + e] = run[ky].get(e);
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const float* wt = smem + ((ci * 3 + ky) * 3 + kx) * COUT;
@@ -665,31 +658,48 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
         }
       }
     }
-    if (DB) {
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        cur[ky] = nxt[ky];
-        cpre[ky] = npre[ky];
-      }
-    }
   }
+  h8 o[PX][COUT / 8];
+#pragma unroll
+  for (int j = 0; j < PX; ++j)
+#pragma unroll
+    for (int c8 = 0; c8 < COUT / 8; ++c8)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = c8 * 8 + e;
+        const float t = acc[j][co] + (co < a.cout ? a.bias[co] : 0.f);
+        o[j][c8][e] = (_Float16)(a.act ? silu(t) : t);
+      }
+  if (a.cout == COUT && a.ycs == COUT) {
+    h8* st = reinterpret_cast<h8*>(smem + nw);  // [256][CPT]
+#pragma unroll
+    for (int j = 0; j < PX; ++j)
+#pragma unroll
+      for (int c8 = 0; c8 < COUT / 8; ++c8) st[threadIdx.x * CPT + j * (COUT / 8) + c8] = o[j][c8];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, t0 = threadIdx.x - lane;  // this wave's first thread
+    const int idx0 = blockIdx.x * 256 + t0;
+    if (idx0 >= nthreads) return;
+    const int row0 = idx0 / Q, q0 = idx0 - row0 * Q;
+    // consecutive threads own consecutive output pixels (Wo % PX == 0), so the wave's output is one
+    // contiguous run of 64 * PX pixels
+    _Float16* y0 = a.y + (int64_t(row0) * a.Wo + PX * q0) * COUT;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int c = k * 64 + lane, tt = c / CPT;
+      if (idx0 + tt < nthreads) reinterpret_cast<h8*>(y0)[c] = st[(t0 + tt) * CPT + (c - tt * CPT)];
+    }
+    return;
+  }
+  if (!valid) return;
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const int ox = PX * q + j;
     if (ox >= a.Wo) break;
     _Float16* yo = a.y + (int64_t(row) * a.Wo + ox) * a.ycs;
 #pragma unroll
-    for (int co0 = 0; co0 < COUT; co0 += 8) {
-      if (co0 >= a.cout) break;
-      h8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int co = co0 + e;
-        const float t = acc[j][co] + (co < a.cout ? a.bias[co] : 0.f);
-        o[e] = (_Float16)(a.act ? silu(t) : t);
-      }
-      *reinterpret_cast<h8*>(yo + co0) = o;
-    }
+    for (int c8 = 0; c8 < COUT / 8; ++c8)
+      if (c8 * 8 < a.cout) *reinterpret_cast<h8*>(yo + c8 * 8) = o[j][c8];
   }
 }
 
@@ -813,24 +823,13 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     int coutT = d.cout <= 16 ? 16 : d.cout <= 32 ? 32 : d.cout <= 64 ? 64 : d.cout <= 96 ? 96 : 0;
     FCE_CHECK(coutT > 0, "stem conv: cout > 96 unsupported");
     const size_t shm = size_t(x.c) * d.k * d.k * coutT * sizeof(float);
-    int PX = coutT <= 16 ? 4 : coutT <= 32 ? 2 : 1, DB = 0;
-    if (const char* e = getenv("FCE_STEM")) {  // diagnostics: "px,db"
-      PX = atoi(e);
-      const char* c = strchr(e, ',');
-      DB = c ? atoi(c + 1) : 0;
-      if (PX != 1 && PX != 2 && PX != 4) PX = 1;
-    }
+    const int PX = coutT <= 32 ? 2 : 1;  // measured: PX 2 beats 4 (occupancy) and 1 (reuse) at cout 16
     if (d.k == 3 && d.stride == 2 && x.c == 3 && x.w % (2 * PX) == 0) {
       const int64_t threads = int64_t(x.n) * Ho * ((Wo + PX - 1) / PX);
       FCE_CHECK(threads < (int64_t(1) << 31), "stem conv: input too large");
       const dim3 grid(unsigned((threads + 255) / 256));
-#define STEM2_LAUNCH(CT, P, T)                                                              \
-  do {                                                                                       \
-    if (DB)                                                                                  \
-      hipLaunchKernelGGL((stem_s2_kernel<CT, P, T, true>), grid, dim3(256), shm, s, a);      \
-    else                                                                                     \
-      hipLaunchKernelGGL((stem_s2_kernel<CT, P, T, false>), grid, dim3(256), shm, s, a);     \
-  } while (0)
+#define STEM2_LAUNCH(CT, P, T)                                                                       \
+  hipLaunchKernelGGL((stem_s2_kernel<CT, P, T>), grid, dim3(256), shm + size_t(256) * P * CT * 2, s, a)
 #define STEM2_DT(CT, P)                  \
   do {                                   \
     if (x.dtype == FCE_F16)              \
@@ -840,23 +839,14 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     else                                 \
       STEM2_LAUNCH(CT, P, uint8_t);      \
   } while (0)
-      if (coutT == 16) {
-        if (PX == 4)
-          STEM2_DT(16, 4);
-        else if (PX == 2)
-          STEM2_DT(16, 2);
-        else
-          STEM2_DT(16, 1);
-      } else if (coutT == 32) {
-        if (PX == 1)
-          STEM2_DT(32, 1);
-        else
-          STEM2_DT(32, 2);
-      } else if (coutT == 64) {
+      if (coutT == 16)
+        STEM2_DT(16, 2);
+      else if (coutT == 32)
+        STEM2_DT(32, 2);
+      else if (coutT == 64)
         STEM2_DT(64, 1);
-      } else {
+      else
         STEM2_DT(96, 1);
-      }
 #undef STEM2_DT
 #undef STEM2_LAUNCH
       return launch_status("stem_s2_kernel");

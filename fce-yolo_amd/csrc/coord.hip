@@ -223,119 +223,6 @@ __global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------- 2+3 fused (BiCoordCrossAtt)
-// One 512-thread block per image does projections, both axial attentions and both output
-// projections with every intermediate in LDS (fce_block.py:236-284): the separate proj / attend
-// launches are latency-bound on these tiny per-image problems.  Used when
-// (H + W) * (C + 4 * mid) floats fit in LDS; same operation order as the unfused kernels.
-struct BiFusedArgs {
-  const float* xh;  // [N][H][C]
-  const float* xw;  // [N][W][C]
-  const float* wt[6];  // [C][mid] transposed: q_h, k_h, v_h, q_w, k_w, v_w
-  const float* b[6];
-  const float* wo[2];  // [mid][oup]: out_h, out_w
-  const float* bo[2];
-  float* g1;  // [N][H][oup]
-  float* g2;  // [N][W][oup]
-  int H, W, C, mid, heads, oup;
-  float scale;
-};
-
-template <int DH>
-__global__ __launch_bounds__(512) void bicoord_fused_kernel(BiFusedArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int n = blockIdx.x, H = a.H, W = a.W, C = a.C, mid = a.mid;
-  float* sxh = sm;                    // H*C
-  float* sxw = sxh + H * C;           // W*C
-  float* qh = sxw + W * C;            // H*mid   (q_h <- x_h)
-  float* kh = qh + H * mid;           // W*mid   (k_h <- x_w)
-  float* vh = kh + W * mid;           // W*mid
-  float* qw = vh + W * mid;           // W*mid   (q_w <- x_w)
-  float* kw = qw + W * mid;           // H*mid   (k_w <- x_h)
-  float* vw = kw + H * mid;           // H*mid
-  float* oh = vw + H * mid;           // H*mid   attention outputs
-  float* ow = oh + H * mid;           // W*mid
-  const float* xhg = a.xh + int64_t(n) * H * C;
-  const float* xwg = a.xw + int64_t(n) * W * C;
-  for (int e = threadIdx.x; e < H * C; e += 512) sxh[e] = xhg[e];
-  for (int e = threadIdx.x; e < W * C; e += 512) sxw[e] = xwg[e];
-  __syncthreads();
-  // six projections: job j reads x_h (L = H) or x_w (L = W)
-  {
-    float* dsts[6] = {qh, kh, vh, qw, kw, vw};
-    const bool from_h[6] = {true, false, false, false, true, true};
-    int base = 0;
-    for (int j = 0; j < 6; ++j) {
-      const int L = from_h[j] ? H : W;
-      const float* src = from_h[j] ? sxh : sxw;
-      const float* wt = a.wt[j];
-      for (int e = threadIdx.x; e < L * mid; e += 512) {
-        const int i = e / mid, m = e - i * mid;
-        const float* s = src + i * C;
-        float acc = a.b[j] ? a.b[j][m] : 0.f;
-        for (int c = 0; c < C; ++c) acc += s[c] * wt[int64_t(c) * mid + m];
-        dsts[j][e] = acc;
-      }
-      base += L * mid;
-    }
-  }
-  __syncthreads();
-  // axial attention, online softmax per (query, head): branch h (queries H, keys W), branch w
-  for (int e = threadIdx.x; e < (H + W) * a.heads; e += 512) {
-    const bool bh = e < H * a.heads;
-    const int ee = bh ? e : e - H * a.heads;
-    const int i = ee / a.heads, hd = ee - i * a.heads;
-    const float* q = (bh ? qh : qw) + i * mid + hd * DH;
-    const float* k = bh ? kh : kw;
-    const float* v = bh ? vh : vw;
-    const int Lk = bh ? W : H;
-    float qv[DH], acc[DH];
-#pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      qv[d] = q[d];
-      acc[d] = 0.f;
-    }
-    float m = -INFINITY, l = 0.f;
-    for (int j = 0; j < Lk; ++j) {
-      const float* kj = k + j * mid + hd * DH;
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) s += qv[d] * kj[d];
-      s *= a.scale;
-      const float mn = fmaxf(m, s);
-      const float corr = expf(m - mn), p = expf(s - mn);
-      l = l * corr + p;
-      const float* vj = v + j * mid + hd * DH;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) acc[d] = acc[d] * corr + p * vj[d];
-      m = mn;
-    }
-    const float inv = 1.0f / l;
-    float* o = (bh ? oh : ow) + i * mid + hd * DH;
-#pragma unroll
-    for (int d = 0; d < DH; ++d) o[d] = acc[d] * inv;
-  }
-  __syncthreads();
-  // output projections -> gates (pre-sigmoid; the apply pass adds g1 + g2)
-  float* g1 = a.g1 + int64_t(n) * H * a.oup;
-  float* g2 = a.g2 + int64_t(n) * W * a.oup;
-  for (int e = threadIdx.x; e < (H + W) * a.oup; e += 512) {
-    const bool bh = e < H * a.oup;
-    const int ee = bh ? e : e - H * a.oup;
-    const int i = ee / a.oup, c = ee - i * a.oup;
-    const float* y = (bh ? oh : ow) + i * mid;
-    const float* wo = a.wo[bh ? 0 : 1];
-    const float* bo = a.bo[bh ? 0 : 1];
-    float acc = bo ? bo[c] : 0.f;
-    for (int m2 = 0; m2 < mid; ++m2) acc += y[m2] * wo[int64_t(m2) * a.oup + c];
-    (bh ? g1 : g2)[ee] = acc;
-  }
-}
-
-static size_t bicoord_fused_lds(int H, int W, int C, int mid) {
-  return (size_t(H + W) * C + size_t(4) * (H + W) * mid) * sizeof(float);
-}
-
 // ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
@@ -443,51 +330,7 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   hipLaunchKernelGGL(pool_cols_kernel, dim3((W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xw);
   int st = launch_status("coord pooling");
   if (st) return st;
-  const size_t fused_lds = bicoord_fused_lds(H, W, C, mid);
-  const int dh = mid / d.heads;
-  const char* fz = getenv("FCE_COORD_FUSED");  // "0": force the generic multi-kernel path (tests)
-  const bool fused_ok = !(fz && atoi(fz) == 0);
-  if (kind == 0 && fused_ok && fused_lds <= 150 * 1024 && (dh == 2 || dh == 4 || dh == 8 || dh == 16)) {
-    BiFusedArgs fa;
-    fa.xh = w.xh;
-    fa.xw = w.xw;
-    for (int i = 0; i < 6; ++i) {
-      fa.wt[i] = d.w[i];
-      fa.b[i] = d.b[i];
-    }
-    fa.wo[0] = d.w[6];
-    fa.wo[1] = d.w[7];
-    fa.bo[0] = d.b[6];
-    fa.bo[1] = d.b[7];
-    fa.g1 = w.g1;
-    fa.g2 = w.g2;
-    fa.H = H;
-    fa.W = W;
-    fa.C = C;
-    fa.mid = mid;
-    fa.heads = d.heads;
-    fa.oup = d.oup;
-    fa.scale = d.scale;
-#define BIF(DH)                                                                                                \
-  do {                                                                                                         \
-    static const bool attr_set = [] {                                                                          \
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(&bicoord_fused_kernel<DH>),                     \
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;        \
-    }();                                                                                                       \
-    (void)attr_set;                                                                                            \
-    hipLaunchKernelGGL(bicoord_fused_kernel<DH>, dim3(N), dim3(512), fused_lds, s, fa);                        \
-  } while (0)
-    if (dh == 2)
-      BIF(2);
-    else if (dh == 4)
-      BIF(4);
-    else if (dh == 8)
-      BIF(8);
-    else
-      BIF(16);
-#undef BIF
-    if ((st = launch_status("bicoord_fused_kernel"))) return st;
-  } else if (kind == 0) {  // BiCoordCrossAtt, generic path
+  if (kind == 0) {  // BiCoordCrossAtt
     ProjJob pj[6] = {
         {w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_NONE_},  // q_h  <- x_h
         {w.xw, d.w[1], d.b[1], w.buf[1], W, C, mid, ACT_NONE_},  // k_h  <- x_w

@@ -32,15 +32,21 @@ def family(name):
 
 
 def load(d, counter):
-    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
-    per = defaultdict(list)
-    for f in files:
+    """Per family: counter bytes of each dispatch of ONE forward — the eager per-op profile pass that
+    bench.py starts right after its marker dispatch (copy_kernel)."""
+    rows = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != counter:
-                continue
-            fam = family(r.get("Kernel_Name", ""))
-            if fam:
-                per[fam].append(float(r["Counter_Value"]) * 1024.0)  # KB -> bytes
+            if r.get("Counter_Name") == counter:
+                rows.append((int(r.get("Dispatch_Id", 0)), r.get("Kernel_Name", ""), float(r["Counter_Value"])))
+    rows.sort()
+    marks = [i for i, (_, name, _) in enumerate(rows) if "copy_kernel" in name]
+    start = marks[-1] + 1 if marks else 0
+    per = defaultdict(list)
+    for _, name, v in rows[start:]:
+        fam = family(name)
+        if fam:
+            per[fam].append(v * 1024.0)  # KB -> bytes
     return per
 
 
@@ -53,7 +59,9 @@ def main(fetch_dir, write_dir):
         fb = 2.0 * sum(f) / max(len(f), 1)  # gfx950: FETCH_SIZE reports half of 16-B/lane reads
         wb = sum(w) / max(len(w), 1)
         out[fam] = {"launches": len(f), "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb}
-    json.dump(out, sys.stdout, indent=1)
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), one forward of bench.py "
+                         "(eager per-op pass); fetch doubled (gfx950 16-B/lane read correction); per launch",
+               "families": out}, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":

@@ -200,17 +200,3 @@ def test_nms_large_candidate_set_global_sort(device):
         od, ok = nms_oracle.non_max_suppression(p, max_nms=max_nms)
         assert np.array_equal(keep[0].cpu().numpy(), ok[0]) and np.array_equal(dets[0].cpu().numpy(), od[0])
 
-
-@pytest.mark.parametrize("name", ["bicoord_n", "bicoord_l_dh16", "bicoord_h8", "bicoord_oup", "bicoord_dh2"])
-def test_bicoord_generic_path_matches_fused(name, ops_fx, device, monkeypatch):
-    """The multi-kernel BiCoordCrossAtt path (large maps that do not fit the fused per-image LDS
-    kernel) against the reference fixture and bitwise against the fused path."""
-    fx = ops_fx.group(name)
-    mod = cases.build_op(name, fx).to(device)
-    x = cases.op_inputs(fx)[0].to(device).half()
-    with torch.no_grad():
-        yf = mod(x).clone()
-        monkeypatch.setenv("FCE_COORD_FUSED", "0")
-        yg = mod(x).clone()
-    assert _rel(yg.float(), torch.from_numpy(fx["out"])) <= OP_TOL
-    assert torch.equal(yf, yg)
