@@ -451,6 +451,64 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
   }
 }
 
+// Row-staged variant: one block = (channel slab of CS <= 64 channels, output row).  The 3 input rows
+// of the slab are staged in LDS with coalesced 16-byte loads; thread e then owns output
+// (pixel e / cg, 8-channel group e % cg), so consecutive lanes store consecutive 16-byte chunks
+// (no partial-line writes).  Per pixel the (ky, kx) order and skipped padding taps match dwconv_kernel.
+template <int S>
+__global__ __launch_bounds__(256) void dwconv_rows_kernel(DwArgs a, int CS) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  const int c0 = blockIdx.x * CS;
+  const int cs = min(CS, a.C - c0), cg = cs >> 3;
+  const int row = blockIdx.y, n = row / a.Ho, oy = row - n * a.Ho;
+  float* wl = dsm;              // [9][CS]
+  float* bl = wl + 9 * CS;      // [CS]
+  h8* rows = reinterpret_cast<h8*>(bl + CS);  // [3][W][CS/8]
+  for (int e = threadIdx.x; e < 9 * cs; e += 256) {
+    const int t = e / cs, c = e - t * cs;
+    wl[t * CS + c] = a.w[t * a.wcs + c0 + c];
+  }
+  for (int c = threadIdx.x; c < cs; c += 256) bl[c] = a.bias[c0 + c];
+  const _Float16* xn = a.x + int64_t(n) * a.H * a.W * a.xcs + c0;
+  const int RW = a.W * (CS >> 3);
+  for (int r = 0; r < 3; ++r) {
+    const int iy = oy * S - 1 + r;
+    const bool rin = iy >= 0 && iy < a.H;
+    for (int e = threadIdx.x; e < a.W * cg; e += 256) {
+      const int xx = e / cg, g = e - xx * cg;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (rin) v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + xx) * a.xcs + 8 * g);
+      rows[r * RW + xx * (CS >> 3) + g] = v;
+    }
+  }
+  __syncthreads();
+  _Float16* yr = a.y + int64_t(row) * a.Wo * a.ycs + c0;
+  for (int e = threadIdx.x; e < a.Wo * cg; e += 256) {
+    const int ox = e / cg, g = e - ox * cg;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = bl[8 * g + j];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * S - 1 + ky;
+      if (iy < 0 || iy >= a.H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * S - 1 + kx;
+        if (ix < 0 || ix >= a.W) continue;
+        const h8 v = rows[ky * RW + ix * (CS >> 3) + g];
+        const float* wt = wl + (ky * 3 + kx) * CS + 8 * g;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j] * wt[j];
+      }
+    }
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
+    *reinterpret_cast<h8*>(yr + int64_t(ox) * a.ycs + 8 * g) = o;
+  }
+}
+
 // depthwise 3x3 (pad 1) on NHWC f16 slices; w = [9][wcs] fp32 taps (BN folded), bias fp32 [C]
 int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
               const fce_tensor& y, hipStream_t s) {
@@ -465,6 +523,17 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
   FCE_CHECK(int64_t(y.n) * Ho < 65536 * 1024, "dwconv: too many output rows");
   DwArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.n, x.h, x.w, x.cstride, x.c, stride, Ho, Wo,
            w, wcs, bias, static_cast<_Float16*>(y.data) + y.coff, y.cstride, act};
+  for (int CS = std::min(64, x.c); CS >= 8; CS /= 2) {  // row-staged kernel while its LDS fits 64 KiB
+    if (CS % 8) continue;
+    const size_t lds = size_t(10) * CS * sizeof(float) + size_t(3) * x.w * CS * sizeof(_Float16);
+    if (lds > 64 * 1024) continue;
+    dim3 g((x.c + CS - 1) / CS, y.n * Ho);
+    if (stride == 1)
+      hipLaunchKernelGGL((dwconv_rows_kernel<1>), g, dim3(256), lds, s, a, CS);
+    else
+      hipLaunchKernelGGL((dwconv_rows_kernel<2>), g, dim3(256), lds, s, a, CS);
+    return launch_status("dwconv_rows_kernel");
+  }
   constexpr int PX = 4;
   dim3 grid(((Wo + PX - 1) / PX * (x.c / 8) + 255) / 256, y.n * Ho);
   if (stride == 1)
