@@ -106,6 +106,7 @@ struct ConvArgs {
   int cpt, nchunk, nsteps;  // K-steps of 32
   int nalloc;               // fragments stored per cout tile (see dense_geom)
   unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
+  int gx, gy;               // logical grid: pixel tiles x cout tiles (launched 1-D, see kernel)
   int vec_ok;
   // fused Detect tail (OUT_DFL / OUT_CLS): pred (N, 4+nc, A) fp32
   float* pred;
@@ -130,8 +131,20 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int wave = threadIdx.x >> 6;
   const int col = lane & 15;
   const int grp = lane >> 4;
-  const int pix_base = (blockIdx.x * 4 + wave) * (RP * 16);
-  const int cot0 = blockIdx.y * RC;
+  // XCD-aware block order.  The grid is 1-D (gx pixel tiles x gy cout tiles); the hardware deals
+  // block b to XCD b % 8.  Remap so each XCD owns one contiguous range of logical tiles
+  // (pixel-tile major, cout tile minor): the cout tiles that re-read a pixel tile's input, and the
+  // neighbouring pixel tiles sharing its 3x3 halo rows, run on the same XCD and hit its L2.
+  int bx, by;
+  {
+    const int total = a.gx * a.gy, b = blockIdx.x;
+    const int per = total >> 3, body = per << 3;
+    const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+    bx = L / a.gy;
+    by = L - bx * a.gy;
+  }
+  const int pix_base = (bx * 4 + wave) * (RP * 16);
+  const int cot0 = by * RC;
   const int cotiles = (a.cout + 15) >> 4;
 
   // Per pixel-rep (this lane's B column): element offset of the tap-(0,0) source pixel, and a
@@ -814,13 +827,16 @@ static void launch_dense(const ConvArgs& a, int out_kind, bool fast, dim3 grid, 
 template <int KS, int RP>
 static void launch_dense_rp(const ConvArgs& a, int out_kind, bool fast, int rc, hipStream_t s) {
   const int cotiles = (a.cout + 15) / 16;
-  dim3 grid((a.P + 64 * RP - 1) / (64 * RP), (cotiles + rc - 1) / rc);
+  ConvArgs b = a;
+  b.gx = (a.P + 64 * RP - 1) / (64 * RP);
+  b.gy = (cotiles + rc - 1) / rc;
+  dim3 grid(unsigned(b.gx * b.gy));
   if (rc == 1)
-    launch_dense<KS, 1, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 1, RP>(b, out_kind, fast, grid, s);
   else if (rc == 2)
-    launch_dense<KS, 2, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 2, RP>(b, out_kind, fast, grid, s);
   else
-    launch_dense<KS, 4, RP>(a, out_kind, fast, grid, s);
+    launch_dense<KS, 4, RP>(b, out_kind, fast, grid, s);
 }
 
 // Tile choice: a wave owns (16*RC couts) x (16*RP pixels).  Big tiles reuse each loaded fragment
