@@ -21,7 +21,7 @@ int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const flo
            const fce_tensor& y, hipStream_t s, int tile = -1);
 int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
                   const fce_detect_epi& e, hipStream_t s, int tile = -1);
-int conv_tile_candidates(const fce_conv_desc& d, int det_box, int* out, int cap);
+int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap);
 int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y2, const fce_tensor& y3, int k,
                   hipStream_t s);
 int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, int accumulate, const fce_tensor& y,
@@ -556,7 +556,8 @@ static int autotune(fce_net* net) {
   for (OpDesc& op : net->ops) {
     if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
     int cand[16];
-    const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0, cand, 16);
+    const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0,
+                                         net->W >> net->bufs[op.in].shift, cand, 16);
     if (nc_ <= 1) continue;
     float best_ms = 1e30f;
     int best = -1;

@@ -523,8 +523,75 @@ __global__ __launch_bounds__(256) void dwconv_rows_kernel(DwArgs a, int CS) {
 }
 
 // depthwise 3x3 (pad 1) on NHWC f16 slices; w = [9][wcs] fp32 taps (BN folded), bias fp32 [C]
+// Lane-contiguous variant: a block owns one output row; thread t = (pixel slot t / cg, group t % cg)
+// with blockDim a multiple of cg, so a thread keeps one channel group (its 9 x 8 weights stay in
+// registers) while striding over the row, and every load / store instruction covers consecutive
+// 16-byte chunks across lanes.
+template <int S>
+__global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
+  const int cg = a.C >> 3;
+  const int tpx = blockDim.x / cg;  // pixels per sweep
+  const int t = threadIdx.x, g = t % cg, px = t / cg;
+  const int row = blockIdx.x, n = row / a.Ho, oy = row - n * a.Ho;
+  const int c0 = g * 8;
+  float wk[9][8], bz[8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const f4 w0 = *reinterpret_cast<const f4*>(a.w + k * a.wcs + c0);
+    const f4 w1 = *reinterpret_cast<const f4*>(a.w + k * a.wcs + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wk[k][j] = w0[j];
+      wk[k][j + 4] = w1[j];
+    }
+  }
+  {
+    const f4 b0 = *reinterpret_cast<const f4*>(a.bias + c0), b1 = *reinterpret_cast<const f4*>(a.bias + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bz[j] = b0[j];
+      bz[j + 4] = b1[j];
+    }
+  }
+  const _Float16* xn = a.x + int64_t(n) * a.H * a.W * a.xcs + c0;
+  _Float16* yr = a.y + int64_t(row) * a.Wo * a.ycs + c0;
+  for (int ox = px; ox < a.Wo; ox += tpx) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = bz[j];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * S - 1 + ky;
+      if (iy < 0 || iy >= a.H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * S - 1 + kx;
+        if (ix < 0 || ix >= a.W) continue;
+        const h8 v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix) * a.xcs);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j] * wk[ky * 3 + kx][j];
+      }
+    }
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
+    *reinterpret_cast<h8*>(yr + int64_t(ox) * a.ycs) = o;
+  }
+}
+
+// Variants (bitwise-identical results; the executor autotunes `variant` per layer, -1 = default):
+//   0 pixel-quad (dwconv_kernel<S,4>)   1 row-staged LDS (dwconv_rows_kernel)   2 lane-contiguous
+int dwconv_variants(int c, int w, int* out, int cap) {
+  int n = 0;
+  if (n < cap) out[n++] = 0;
+  if (n < cap && size_t(10) * 8 * sizeof(float) + size_t(3) * w * 8 * sizeof(_Float16) <= 64 * 1024) out[n++] = 1;
+  if (n < cap && c / 8 <= 256) out[n++] = 2;
+  return n;
+}
+
+// depthwise 3x3 (pad 1) on NHWC f16 slices; w = [9][wcs] fp32 taps (BN folded), bias fp32 [C]
 int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
-              const fce_tensor& y, hipStream_t s) {
+              const fce_tensor& y, hipStream_t s, int variant) {
   FCE_CHECK(x.c == y.c && x.c % 8 == 0 && wcs >= x.c && wcs % 4 == 0, "dwconv: channel mismatch");
   FCE_CHECK(x.layout == FCE_NHWC && y.layout == FCE_NHWC && x.dtype == FCE_F16 && y.dtype == FCE_F16,
             "dwconv: NHWC f16 views");
@@ -536,16 +603,28 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
   FCE_CHECK(int64_t(y.n) * Ho < 65536 * 1024, "dwconv: too many output rows");
   DwArgs a{static_cast<const _Float16*>(x.data) + x.coff, x.n, x.h, x.w, x.cstride, x.c, stride, Ho, Wo,
            w, wcs, bias, static_cast<_Float16*>(y.data) + y.coff, y.cstride, act};
-  for (int CS = std::min(64, x.c); CS >= 8; CS /= 2) {  // row-staged kernel while its LDS fits 64 KiB
-    if (CS % 8) continue;
-    const size_t lds = size_t(10) * CS * sizeof(float) + size_t(3) * x.w * CS * sizeof(_Float16);
-    if (lds > 64 * 1024) continue;
-    dim3 g((x.c + CS - 1) / CS, y.n * Ho);
+  if (variant < 0) variant = 0;
+  if (variant == 1) {
+    for (int CS = std::min(64, x.c); CS >= 8; CS /= 2) {  // row-staged kernel while its LDS fits 64 KiB
+      if (CS % 8) continue;
+      const size_t lds = size_t(10) * CS * sizeof(float) + size_t(3) * x.w * CS * sizeof(_Float16);
+      if (lds > 64 * 1024) continue;
+      dim3 g((x.c + CS - 1) / CS, y.n * Ho);
+      if (stride == 1)
+        hipLaunchKernelGGL((dwconv_rows_kernel<1>), g, dim3(256), lds, s, a, CS);
+      else
+        hipLaunchKernelGGL((dwconv_rows_kernel<2>), g, dim3(256), lds, s, a, CS);
+      return launch_status("dwconv_rows_kernel");
+    }
+  }
+  if (variant == 2 && x.c / 8 <= 256) {
+    const int cg = x.c / 8;
+    const int threads = (256 / cg) * cg;
     if (stride == 1)
-      hipLaunchKernelGGL((dwconv_rows_kernel<1>), g, dim3(256), lds, s, a, CS);
+      hipLaunchKernelGGL((dwconv_lanes_kernel<1>), dim3(y.n * Ho), dim3(threads), 0, s, a);
     else
-      hipLaunchKernelGGL((dwconv_rows_kernel<2>), g, dim3(256), lds, s, a, CS);
-    return launch_status("dwconv_rows_kernel");
+      hipLaunchKernelGGL((dwconv_lanes_kernel<2>), dim3(y.n * Ho), dim3(threads), 0, s, a);
+    return launch_status("dwconv_lanes_kernel");
   }
   constexpr int PX = 4;
   dim3 grid(((Wo + PX - 1) / PX * (x.c / 8) + 255) / 256, y.n * Ho);
@@ -870,11 +949,18 @@ static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, 
     launch_dense_rp<KS, 4>(a, out_kind, fast, rc, s);
 }
 
-// Register tiles a dense conv may run with, encoded rc | rp << 4 (the executor times them at plan
-// time and keeps the fastest; the tile never changes the K summation order, so results are bitwise
-// the same for every choice).  Returns the count; 0 for stem / depthwise convs.
-int conv_tile_candidates(const fce_conv_desc& d, int det_box, int* out, int cap) {
-  if (is_stem(d) || is_dw(d)) return 0;
+// Register tiles a dense conv may run with, encoded rc | rp << 4, or depthwise kernel variants,
+// encoded 100 + variant (the executor times them at plan time and keeps the fastest; neither
+// changes the per-output summation order, so results are bitwise the same for every choice).
+// Returns the count; 0 for the stem.
+int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap) {
+  if (is_stem(d)) return 0;
+  if (is_dw(d)) {  // depthwise kernel variants, coded 100 + variant
+    int v[4];
+    const int nv = d.k == 3 ? dwconv_variants(d.cin, in_w, v, 4) : 0;
+    for (int i = 0; i < nv && i < cap; ++i) out[i] = 100 + v[i];
+    return std::min(nv, cap);
+  }
   const int cotiles = (d.cout + 15) / 16;
   int n = 0;
   for (int rc : {1, 2, 4}) {
@@ -966,7 +1052,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     FCE_CHECK(d.groups == d.cin && d.cin == d.cout && d.cin % 8 == 0, "dwconv: groups == cin == cout, cin % 8 == 0");
     FCE_CHECK(y.dtype == FCE_F16 && d.up == 0 && res == nullptr && d.epilogue == FCE_EPI_STORE && d.k == 3,
               "dwconv: 3x3, plain f16 store only");
-    return dwconv3x3(x, d.stride, static_cast<const float*>(w), d.cin, bias, d.act, y, s);
+    return dwconv3x3(x, d.stride, static_cast<const float*>(w), d.cin, bias, d.act, y, s, tile >= 100 ? tile - 100 : -1);
   }
 
   FCE_CHECK(d.cin % 8 == 0, "conv: cin must be a multiple of 8");

@@ -20,7 +20,7 @@
 namespace fce {
 
 int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
-              const fce_tensor& y, hipStream_t s);
+              const fce_tensor& y, hipStream_t s, int variant = -1);
 
 template <int KD, int HD>
 __global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
