@@ -128,8 +128,9 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return act == ACT_SILU_ ? v / (1.0f + expf(-v)) : act == ACT_SIGMOID_ ? 1.0f / (1.0f + expf(-v)) : v;
 }
 
-// grid (position tiles, jobs, N); tile of TP positions staged in LDS
-__global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP) {
+// grid (position tiles, jobs, N); tile of TP positions staged in LDS, and the [K][M] weight matrix
+// too when it fits (wlds): the K-long dot products then run from LDS instead of a chain of L2 loads.
+__global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP, int wlds) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const ProjJob& jb = pa.job[blockIdx.y];
   const int n = blockIdx.z;
@@ -138,13 +139,19 @@ __global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP) {
   const int np = min(TP, jb.L - p0);
   const float* src = jb.src + (int64_t(n) * jb.L + p0) * jb.K;
   for (int e = threadIdx.x; e < np * jb.K; e += blockDim.x) sm[e] = src[e];
+  const float* wt = jb.wt;
+  if (wlds) {
+    float* ws = sm + TP * jb.K;
+    for (int e = threadIdx.x; e < jb.K * jb.M; e += blockDim.x) ws[e] = jb.wt[e];
+    wt = ws;
+  }
   __syncthreads();
   float* dst = jb.dst + (int64_t(n) * jb.L + p0) * jb.M;
   for (int e = threadIdx.x; e < np * jb.M; e += blockDim.x) {
     const int i = e / jb.M, m = e - (e / jb.M) * jb.M;
     const float* s = sm + i * jb.K;
     float acc = jb.b ? jb.b[m] : 0.f;
-    for (int c = 0; c < jb.K; ++c) acc += s[c] * jb.wt[int64_t(c) * jb.M + m];
+    for (int c = 0; c < jb.K; ++c) acc += s[c] * wt[c * jb.M + m];
     dst[e] = act_f(acc, jb.act);
   }
 }
@@ -163,6 +170,7 @@ struct AttArgs {
   AttJob job[2];
   int mid, heads, oup, QT;
   float scale;
+  int wlds;  // output-projection weights staged in LDS
 };
 
 template <int DH>
@@ -176,11 +184,17 @@ __global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
   float* ks = sm;                 // Lk*mid
   float* vs = ks + Lk * mid;      // Lk*mid
   float* ys = vs + Lk * mid;      // QT*mid
+  float* wo = ys + a.QT * mid;    // [mid][oup] output projection (when a.wlds)
   const float* kg = jb.k + int64_t(n) * Lk * mid;
   const float* vg = jb.v + int64_t(n) * Lk * mid;
   for (int e = threadIdx.x; e < Lk * mid; e += blockDim.x) {
     ks[e] = kg[e];
     vs[e] = vg[e];
+  }
+  const float* wt = jb.wt;
+  if (a.wlds) {
+    for (int e = threadIdx.x; e < mid * a.oup; e += blockDim.x) wo[e] = jb.wt[e];
+    wt = wo;
   }
   __syncthreads();
   const int nq = min(a.QT, jb.Lq - i0);
@@ -218,7 +232,7 @@ __global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
     const int il = e / a.oup, c = e - il * a.oup;
     const float* y = ys + il * mid;
     float acc = jb.b ? jb.b[c] : 0.f;
-    for (int m2 = 0; m2 < mid; ++m2) acc += y[m2] * jb.wt[int64_t(m2) * a.oup + c];
+    for (int m2 = 0; m2 < mid; ++m2) acc += y[m2] * wt[m2 * a.oup + c];
     dst[e] = act_f(acc, jb.act);
   }
 }
@@ -226,15 +240,17 @@ __global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
 // ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
+// grid (row chunks, N*H): thread = (column, 8-channel group) of one row, 32-bit index math
 template <int MODE>
 __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int xcs, _Float16* y, int ycs, int N,
                                                          int H, int W, int C, const float* g1, const float* g2) {
   const int CG = C / 8;
-  const int64_t total = int64_t(N) * H * W * CG;
-  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
-    const int g = int(t % CG);
-    const int64_t pix = t / CG;
-    const int xx = int(pix % W), yy = int((pix / W) % H), n = int(pix / (int64_t(W) * H));
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= W * CG) return;
+  {
+    const int xx = e / CG, g = e - xx * CG;
+    const int row = blockIdx.y, n = row / H, yy = row - n * H;
+    const int64_t pix = int64_t(row) * W + xx;
     const h8 v = *reinterpret_cast<const h8*>(x + pix * xcs + g * 8);
     const float* gh = g1 + (int64_t(n) * H + yy) * C + g * 8;
     const f4 gh0 = *reinterpret_cast<const f4*>(gh), gh1 = *reinterpret_cast<const f4*>(gh + 4);
@@ -262,6 +278,7 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
   }
 }
 
+
 // ---------------------------------------------------------------------------- host
 static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
   ProjArgs pa;
@@ -272,8 +289,12 @@ static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
     maxK = std::max(maxK, jobs[i].K);
   }
   const int TP = std::max(1, std::min(16, 8192 / maxK));
+  int maxKM = 0;
+  for (int i = 0; i < nj; ++i) maxKM = std::max(maxKM, jobs[i].K * jobs[i].M);
+  const int wlds = (size_t(TP) * maxK + maxKM) * sizeof(float) <= 64 * 1024;
   dim3 grid((maxL + TP - 1) / TP, nj, N);
-  hipLaunchKernelGGL(coord_proj_kernel, grid, dim3(256), size_t(TP) * maxK * sizeof(float), s, pa, TP);
+  hipLaunchKernelGGL(coord_proj_kernel, grid, dim3(256), (size_t(TP) * maxK + (wlds ? maxKM : 0)) * sizeof(float), s,
+                     pa, TP, wlds);
   return launch_status("coord_proj_kernel");
 }
 
@@ -290,14 +311,23 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
     maxLq = std::max(maxLq, jobs[i].Lq);
     maxLk = std::max(maxLk, jobs[i].Lk);
   }
-  const size_t shm = (size_t(2) * maxLk * d.mid + size_t(a.QT) * d.mid) * sizeof(float);
-  if (shm > 160 * 1024) return fail(FCE_ERR_UNSUPPORTED, "coord attention: K/V do not fit in LDS");
+  constexpr size_t kMaxLds = 160 * 1024;  // gfx950 LDS per workgroup (opted in below)
+  size_t shm = (size_t(2) * maxLk * d.mid + size_t(a.QT) * d.mid) * sizeof(float);
+  if (shm > kMaxLds) return fail(FCE_ERR_UNSUPPORTED, "coord attention: K/V do not fit in LDS");
+  a.wlds = shm + size_t(d.mid) * d.oup * sizeof(float) <= kMaxLds;
+  if (a.wlds) shm += size_t(d.mid) * d.oup * sizeof(float);
   dim3 grid((maxLq + a.QT - 1) / a.QT, nj, N);
   const int dh = d.mid / d.heads;
   switch (dh) {
-#define ATT(DH) \
-  case DH:      \
-    hipLaunchKernelGGL(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a); break;
+#define ATT(DH)                                                                                         \
+  case DH: {                                                                                            \
+    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&coord_attend_kernel<DH>), \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                                    int(kMaxLds)) == hipSuccess;                        \
+    if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord attention: cannot opt in to >64 KiB LDS"); \
+    hipLaunchKernelGGL(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a);                            \
+    break;                                                                                              \
+  }
     ATT(1) ATT(2) ATT(3) ATT(4) ATT(5) ATT(6) ATT(7) ATT(8) ATT(10) ATT(12) ATT(16) ATT(20) ATT(24) ATT(32)
     ATT(48) ATT(64)
 #undef ATT
@@ -372,17 +402,17 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
     scs = y.cstride;
   }
   _Float16* yp = static_cast<_Float16*>(y.data) + y.coff;
-  const int64_t total = int64_t(N) * H * W * (d.oup / 8);
-  const int blocks = int(std::min<int64_t>((total + 255) / 256, 65535 * 8));
+  FCE_CHECK(int64_t(N) * H < 65536 * 1024, "coord attention: too many rows");
+  const dim3 grid((W * (d.oup / 8) + 255) / 256, N * H);
   if (kind == 0)
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_BICOORD>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H,
-                       W, d.oup, w.g1, w.g2);
-  else if (kind == 1)
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_COORD>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H,
-                       W, d.oup, w.g1, w.g2);
-  else
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_ROW>, dim3(blocks), dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
+    hipLaunchKernelGGL(gate_apply_kernel<GATE_BICOORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
                        d.oup, w.g1, w.g2);
+  else if (kind == 1)
+    hipLaunchKernelGGL(gate_apply_kernel<GATE_COORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+                       w.g1, w.g2);
+  else
+    hipLaunchKernelGGL(gate_apply_kernel<GATE_ROW>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+                       w.g1, w.g2);
   return launch_status("gate_apply_kernel");
 }
 
