@@ -197,6 +197,19 @@ struct fce_net {
   float* cap_out = nullptr;
   hipStream_t cap_stream = nullptr;
   fce_tensor cap_desc{};
+  // multi-stream capture: side streams + one event per op (+ fork), created on first capture
+  std::vector<hipStream_t> side;
+  std::vector<hipEvent_t> op_ev;
+  hipEvent_t fork_ev = nullptr;
+
+  void drop_streams() {
+    for (hipEvent_t e : op_ev) (void)hipEventDestroy(e);
+    op_ev.clear();
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    fork_ev = nullptr;
+    for (hipStream_t q : side) (void)hipStreamDestroy(q);
+    side.clear();
+  }
 
   void drop_graph() {
     if (exec) (void)hipGraphExecDestroy(exec);
@@ -214,7 +227,10 @@ struct fce_net {
     ws = nullptr;
     arena_bytes = ws_bytes = 0;
   }
-  ~fce_net() { release(); }
+  ~fce_net() {
+    release();
+    drop_streams();
+  }
 
   fce_tensor view(int id, int coff, int c) const {
     const BufDesc& b = bufs[id];
@@ -299,6 +315,113 @@ int run_all(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s) {
     int st = run_op(net, op, input, pred, s);
     if (st) return st;
   }
+  return FCE_OK;
+}
+
+// ---- dependency DAG for multi-stream graph capture
+// Every op touches buffer channel ranges (reads / writes); two ops conflict when they touch
+// overlapping ranges of the same buffer and at least one writes.  The coordinate-attention ops
+// share the executor workspace (pseudo buffer WS); Detect tails write disjoint blocks of pred.
+struct Access {
+  int buf, c0, c1;
+  bool write;
+};
+static constexpr int kBufPred = -2, kBufWs = -3;
+
+static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access>& a) {
+  a.clear();
+  switch (op.kind) {
+    case OP_CONV:
+      if (op.in >= 0) a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
+      if (op.res >= 0) a.push_back({op.res, op.res_coff, op.res_coff + op.conv.cout, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.conv.cout, true});
+      break;
+    case OP_MAXPOOL:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.in_c, false});
+      a.push_back({op.in, op.in_coff + op.in_c, op.in_coff + 4 * op.in_c, true});
+      break;
+    case OP_WADD:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.in_c, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.in_c, true});
+      break;
+    case OP_COORD:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.coord.inp, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.coord.oup, true});
+      a.push_back({kBufWs, 0, 1, true});
+      break;
+    case OP_PSA:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.in_c, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.heads * op.head_dim, true});
+      break;
+    case OP_CONV_DETECT:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
+      a.push_back({kBufPred, 2 * op.level + op.part, 2 * op.level + op.part + 1, true});
+      break;
+    case OP_DETECT:
+      for (int i = 0; i < op.nl; ++i) a.push_back({op.box[i], 0, net->bufs[op.box[i]].c, false});
+      a.push_back({kBufPred, 0, 1 << 20, true});
+      break;
+  }
+}
+
+static bool conflict(const std::vector<Access>& x, const std::vector<Access>& y) {
+  for (const Access& p : x)
+    for (const Access& q : y)
+      if (p.buf == q.buf && (p.write || q.write) && p.c0 < q.c1 && q.c0 < p.c1) return true;
+  return false;
+}
+
+// Capture-time scheduling of the op DAG onto the capturing stream + side streams: an op goes to the
+// stream of its most recent dependency when that stream has not moved on, otherwise to the stream
+// idle longest, and waits (hipStreamWaitEvent) on every dependency recorded on another stream.
+// The captured hipGraph then holds the true dependencies, so independent branches (the Detect
+// levels / box and cls chains, the head of P3 against the neck's P4/P5 path) run concurrently.
+int run_all_streams(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s, int nstreams) {
+  const int nops = int(net->ops.size());
+  while (int(net->side.size()) < nstreams - 1) {
+    hipStream_t q = nullptr;
+    FCE_HIP_CHECK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+    net->side.push_back(q);
+  }
+  while (int(net->op_ev.size()) < nops) {
+    hipEvent_t e = nullptr;
+    FCE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    net->op_ev.push_back(e);
+  }
+  if (!net->fork_ev) FCE_HIP_CHECK(hipEventCreateWithFlags(&net->fork_ev, hipEventDisableTiming));
+  std::vector<hipStream_t> st(nstreams);
+  st[0] = s;
+  for (int k = 1; k < nstreams; ++k) st[k] = net->side[k - 1];
+  FCE_HIP_CHECK(hipEventRecord(net->fork_ev, s));
+  for (int k = 1; k < nstreams; ++k) FCE_HIP_CHECK(hipStreamWaitEvent(st[k], net->fork_ev, 0));
+  std::vector<std::vector<Access>> acc(nops);
+  for (int j = 0; j < nops; ++j) op_accesses(net, net->ops[j], acc[j]);
+  std::vector<int> stream_of(nops, 0), last_on(nstreams, -1);
+  std::vector<int> deps;
+  for (int j = 0; j < nops; ++j) {
+    deps.clear();
+    for (int i = 0; i < j; ++i)
+      if (conflict(acc[i], acc[j])) deps.push_back(i);
+    int pick = -1;
+    for (int t = int(deps.size()) - 1; t >= 0 && pick < 0; --t) {
+      const int k = stream_of[deps[t]];
+      if (last_on[k] == deps[t]) pick = k;  // continue the chain on its own stream
+    }
+    if (pick < 0) {  // the stream whose last op is oldest
+      pick = 0;
+      for (int k = 1; k < nstreams; ++k)
+        if (last_on[k] < last_on[pick]) pick = k;
+    }
+    for (int i : deps)
+      if (stream_of[i] != pick || i > last_on[pick]) FCE_HIP_CHECK(hipStreamWaitEvent(st[pick], net->op_ev[i], 0));
+    const int rc = run_op(net, net->ops[j], input, pred, st[pick]);
+    if (rc) return rc;
+    FCE_HIP_CHECK(hipEventRecord(net->op_ev[j], st[pick]));
+    stream_of[j] = pick;
+    last_on[pick] = j;
+  }
+  for (int k = 1; k < nstreams; ++k)
+    if (last_on[k] >= 0) FCE_HIP_CHECK(hipStreamWaitEvent(s, net->op_ev[last_on[k]], 0));
   return FCE_OK;
 }
 
@@ -654,8 +777,10 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
                       net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c;
     if (!same) {
       net->drop_graph();
+      const char* ns = getenv("FCE_STREAMS");  // graph branches run on up to this many streams (1 = linear)
+      const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 4));
       FCE_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      st = run_all(net, *input, pred, s);
+      st = nstreams > 1 ? run_all_streams(net, *input, pred, s, nstreams) : run_all(net, *input, pred, s);
       hipGraph_t g = nullptr;
       hipError_t e = hipStreamEndCapture(s, &g);
       if (st) {
