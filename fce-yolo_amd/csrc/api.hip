@@ -201,6 +201,9 @@ struct fce_net {
   std::vector<hipStream_t> side;
   std::vector<hipEvent_t> op_ev;
   hipEvent_t fork_ev = nullptr;
+  int cap_nstreams = 0;
+  hipStream_t own = nullptr;                   // capture/replay stream when the caller passes the null stream
+  hipEvent_t join_ev[2] = {nullptr, nullptr};  // caller -> own, own -> caller
 
   void drop_streams() {
     for (hipEvent_t e : op_ev) (void)hipEventDestroy(e);
@@ -209,6 +212,12 @@ struct fce_net {
     fork_ev = nullptr;
     for (hipStream_t q : side) (void)hipStreamDestroy(q);
     side.clear();
+    for (hipEvent_t& e : join_ev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    if (own) (void)hipStreamDestroy(own);
+    own = nullptr;
   }
 
   void drop_graph() {
@@ -770,15 +779,29 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
   FCE_CHECK(net && pred, "fce_net_forward: null argument");
   int st = check_input(net, input);
   if (st) return st;
-  hipStream_t s = S(stream);
+  hipStream_t caller = S(stream);
   FCE_GUARD({
-    if (!graph || s == nullptr) return run_all(net, *input, pred, s);
+    const char* ns = getenv("FCE_STREAMS");  // graph branches run on up to this many streams (1 = linear)
+    const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 4));
+    if (!graph) return run_all(net, *input, pred, caller);
+    // The legacy null stream cannot be captured: the net then captures and replays on a stream of
+    // its own, ordered after / before the caller's stream with events.
+    hipStream_t s = caller;
+    if (s == nullptr) {
+      if (!net->own) FCE_HIP_CHECK(hipStreamCreateWithFlags(&net->own, hipStreamNonBlocking));
+      if (!net->join_ev[0]) {
+        FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[0], hipEventDisableTiming));
+        FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[1], hipEventDisableTiming));
+      }
+      s = net->own;
+      FCE_HIP_CHECK(hipEventRecord(net->join_ev[0], caller));
+      FCE_HIP_CHECK(hipStreamWaitEvent(s, net->join_ev[0], 0));
+    }
     const bool same = net->exec && net->cap_in == input->data && net->cap_out == pred && net->cap_stream == s &&
-                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c;
+                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c &&
+                      net->cap_nstreams == nstreams;
     if (!same) {
       net->drop_graph();
-      const char* ns = getenv("FCE_STREAMS");  // graph branches run on up to this many streams (1 = linear)
-      const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 4));
       FCE_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       st = nstreams > 1 ? run_all_streams(net, *input, pred, s, nstreams) : run_all(net, *input, pred, s);
       hipGraph_t g = nullptr;
@@ -794,8 +817,13 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
       net->cap_out = pred;
       net->cap_stream = s;
       net->cap_desc = *input;
+      net->cap_nstreams = nstreams;
     }
     FCE_HIP_CHECK(hipGraphLaunch(net->exec, s));
+    if (s != caller) {
+      FCE_HIP_CHECK(hipEventRecord(net->join_ev[1], s));
+      FCE_HIP_CHECK(hipStreamWaitEvent(caller, net->join_ev[1], 0));
+    }
     return FCE_OK;
   })
 }
