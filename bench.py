@@ -71,6 +71,8 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
+    ap.add_argument("--graph", type=int, default=1, help="1: replay a captured hipGraph; 0: direct launches "
+                    "(op DAG over FCE_STREAMS streams)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     return ap.parse_args()
@@ -126,7 +128,7 @@ def main():
 
     B, S = a.batch, a.imgsz
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
-    eng = Engine(model, B, S, dev)
+    eng = Engine(model, B, S, dev, graph=bool(a.graph))
     nms = NMS(B, eng.anchors, eng.nc, dev)
 
     def step():

@@ -201,7 +201,6 @@ struct fce_net {
   std::vector<hipStream_t> side;
   std::vector<hipEvent_t> op_ev;
   hipEvent_t fork_ev = nullptr;
-  int cap_nstreams = 0;
   hipStream_t own = nullptr;                   // capture/replay stream when the caller passes the null stream
   hipEvent_t join_ev[2] = {nullptr, nullptr};  // caller -> own, own -> caller
 
@@ -380,14 +379,15 @@ static bool conflict(const std::vector<Access>& x, const std::vector<Access>& y)
   return false;
 }
 
-// Capture-time scheduling of the op DAG onto the capturing stream + side streams: an op goes to the
-// stream of its most recent dependency when that stream has not moved on, otherwise to the stream
-// idle longest, and waits (hipStreamWaitEvent) on every dependency recorded on another stream.
-// The captured hipGraph then holds the true dependencies, so independent branches (the Detect
-// levels / box and cls chains, the head of P3 against the neck's P4/P5 path) run concurrently.
+// Scheduling of the op DAG onto the net's streams: an op goes to the stream of its most recent
+// dependency when that stream has not moved on, otherwise to the stream idle longest, and waits
+// (hipStreamWaitEvent) on every dependency recorded on another stream, so independent branches (the
+// Detect levels / box and cls chains, the P3 head against the neck's P4/P5 path) run concurrently.
+// Launched directly: multi-stream stream capture crashed the ROCm 7 runtime here (4 streams), and a
+// captured linear graph replays slower than direct launches (measured).
 int run_all_streams(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s, int nstreams) {
   const int nops = int(net->ops.size());
-  while (int(net->side.size()) < nstreams - 1) {
+  while (int(net->side.size()) < nstreams) {
     hipStream_t q = nullptr;
     FCE_HIP_CHECK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
     net->side.push_back(q);
@@ -398,11 +398,9 @@ int run_all_streams(fce_net* net, const fce_tensor& input, float* pred, hipStrea
     net->op_ev.push_back(e);
   }
   if (!net->fork_ev) FCE_HIP_CHECK(hipEventCreateWithFlags(&net->fork_ev, hipEventDisableTiming));
-  std::vector<hipStream_t> st(nstreams);
-  st[0] = s;
-  for (int k = 1; k < nstreams; ++k) st[k] = net->side[k - 1];
+  std::vector<hipStream_t> st(net->side.begin(), net->side.begin() + nstreams);
   FCE_HIP_CHECK(hipEventRecord(net->fork_ev, s));
-  for (int k = 1; k < nstreams; ++k) FCE_HIP_CHECK(hipStreamWaitEvent(st[k], net->fork_ev, 0));
+  for (int k = 0; k < nstreams; ++k) FCE_HIP_CHECK(hipStreamWaitEvent(st[k], net->fork_ev, 0));
   std::vector<std::vector<Access>> acc(nops);
   for (int j = 0; j < nops; ++j) op_accesses(net, net->ops[j], acc[j]);
   std::vector<int> stream_of(nops, 0), last_on(nstreams, -1);
@@ -429,7 +427,7 @@ int run_all_streams(fce_net* net, const fce_tensor& input, float* pred, hipStrea
     stream_of[j] = pick;
     last_on[pick] = j;
   }
-  for (int k = 1; k < nstreams; ++k)
+  for (int k = 0; k < nstreams; ++k)
     if (last_on[k] >= 0) FCE_HIP_CHECK(hipStreamWaitEvent(s, net->op_ev[last_on[k]], 0));
   return FCE_OK;
 }
@@ -781,29 +779,33 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
   if (st) return st;
   hipStream_t caller = S(stream);
   FCE_GUARD({
-    const char* ns = getenv("FCE_STREAMS");  // graph branches run on up to this many streams (1 = linear)
-    const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 4));
-    if (!graph) return run_all(net, *input, pred, caller);
-    // The legacy null stream cannot be captured: the net then captures and replays on a stream of
-    // its own, ordered after / before the caller's stream with events.
+    if (!graph) {
+      // direct launches; the op DAG is spread over FCE_STREAMS (default 4) streams of the net's own,
+      // forked from and joined back to the caller's stream with events
+      const char* ns = getenv("FCE_STREAMS");
+      const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 4));
+      if (nstreams == 1) return run_all(net, *input, pred, caller);
+      return run_all_streams(net, *input, pred, caller, nstreams);
+    }
+    // hipGraph: one linear capture (the legacy null stream cannot be captured, so the net then
+    // captures and replays on a stream of its own, ordered against the caller's with events)
     hipStream_t s = caller;
+    if (!net->join_ev[0]) {
+      FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[0], hipEventDisableTiming));
+      FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[1], hipEventDisableTiming));
+    }
     if (s == nullptr) {
       if (!net->own) FCE_HIP_CHECK(hipStreamCreateWithFlags(&net->own, hipStreamNonBlocking));
-      if (!net->join_ev[0]) {
-        FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[0], hipEventDisableTiming));
-        FCE_HIP_CHECK(hipEventCreateWithFlags(&net->join_ev[1], hipEventDisableTiming));
-      }
       s = net->own;
       FCE_HIP_CHECK(hipEventRecord(net->join_ev[0], caller));
       FCE_HIP_CHECK(hipStreamWaitEvent(s, net->join_ev[0], 0));
     }
     const bool same = net->exec && net->cap_in == input->data && net->cap_out == pred && net->cap_stream == s &&
-                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c &&
-                      net->cap_nstreams == nstreams;
+                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c;
     if (!same) {
       net->drop_graph();
       FCE_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      st = nstreams > 1 ? run_all_streams(net, *input, pred, s, nstreams) : run_all(net, *input, pred, s);
+      st = run_all(net, *input, pred, s);
       hipGraph_t g = nullptr;
       hipError_t e = hipStreamEndCapture(s, &g);
       if (st) {
@@ -817,7 +819,6 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
       net->cap_out = pred;
       net->cap_stream = s;
       net->cap_desc = *input;
-      net->cap_nstreams = nstreams;
     }
     FCE_HIP_CHECK(hipGraphLaunch(net->exec, s));
     if (s != caller) {
