@@ -71,8 +71,8 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
-    ap.add_argument("--graph", type=int, default=1, help="1: replay a captured hipGraph; 0: direct launches "
-                    "(op DAG over FCE_STREAMS streams)")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay a captured hipGraph; 0: direct launches "
+                    "(measured faster on ROCm 7.2, DESIGN.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     return ap.parse_args()

@@ -21,7 +21,7 @@ _DT = {torch.float16: N.F16, torch.float32: N.F32, torch.uint8: N.U8}
 
 
 class Engine:
-    def __init__(self, model, batch: int, imgsz: int | tuple[int, int], device=None, graph: bool = True):
+    def __init__(self, model, batch: int, imgsz: int | tuple[int, int], device=None, graph: bool = False):
         if isinstance(imgsz, int):
             imgsz = (imgsz, imgsz)
         self.H, self.W = imgsz

@@ -121,15 +121,19 @@ def test_end_to_end_parity(key, e2e_fx, device):
     assert box <= BOX_TOL and cls <= CLS_TOL, (box, cls)
 
 
-def test_graph_eager_and_module_forward_agree_bitwise(e2e_fx, device):
+def test_graph_eager_and_module_forward_agree_bitwise(e2e_fx, device, monkeypatch):
+    """Captured hipGraph, direct launches (1 and 4 streams over the op DAG) and the module forward."""
     key = "yolo11n-fce_160_b2"
     fx = e2e_fx.group(key)
     model, eng, x, yg = _engine_run(key, fx, device, graph=True)
     ye = eng(x.to(device).half(), graph=False).clone()
     yg2 = eng(x.to(device).half(), graph=True).clone()  # replay
+    monkeypatch.setenv("FCE_STREAMS", "4")
+    ys = eng(x.to(device).half(), graph=False).clone()
+    monkeypatch.delenv("FCE_STREAMS")
     ym, _ = model(x.to(device).half())
     torch.cuda.synchronize()
-    assert torch.equal(yg, ye) and torch.equal(yg, yg2) and torch.equal(yg, ym)
+    assert torch.equal(yg, ye) and torch.equal(yg, yg2) and torch.equal(yg, ym) and torch.equal(yg, ys)
 
 
 def test_batch_invariance_640(device):
