@@ -685,9 +685,9 @@ static int autotune(fce_net* net) {
   fce_tensor none{};
   for (OpDesc& op : net->ops) {
     if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
-    int cand[16];
+    int cand[32];
     const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0,
-                                         net->W >> net->bufs[op.in].shift, cand, 16);
+                                         net->W >> net->bufs[op.in].shift, cand, 32);
     if (nc_ <= 1) continue;
     float best_ms = 1e30f;
     int best = -1;

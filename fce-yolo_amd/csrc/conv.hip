@@ -62,20 +62,32 @@ int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
       for (int t = 0; t < kk; ++t) o[t * d.cin + c] = w[c * kk + t];
     return FCE_OK;
   }
+  // K-step order: cin % 32 == 0 -> chunk-major, step s = (32-channel chunk) * k*k + tap (the order
+  // of the LDS-tile 3x3 kernel, so both kernels sum every output in the same order); otherwise
+  // 8-channel chunks c = 4s + lane/16 in tap-major order (tap = c / (cin/8)).
   DenseGeom g = dense_geom(d);
+  const bool chunk_major = d.cin % 32 == 0;
   _Float16* o = static_cast<_Float16*>(out);
   for (int ct = 0; ct < g.cotiles; ++ct)
     for (int s = 0; s < g.nalloc; ++s)
       for (int l = 0; l < 64; ++l) {
         const int co = ct * 16 + (l & 15);
-        const int c = s * 4 + (l >> 4);
         _Float16* dst = o + ((size_t(ct) * g.nalloc + s) * 64 + l) * 8;
+        int tap, ci0;
+        bool in;
+        if (chunk_major) {
+          tap = s % kk;
+          ci0 = (s / kk) * 32 + (l >> 4) * 8;
+          in = s < g.nsteps;
+        } else {
+          const int c = s * 4 + (l >> 4);
+          tap = c / g.cpt;
+          ci0 = (c % g.cpt) * 8;
+          in = c < g.nchunk;
+        }
         for (int j = 0; j < 8; ++j) {
           float v = 0.f;
-          if (co < d.cout && c < g.nchunk) {
-            const int tap = c / g.cpt, ci = (c % g.cpt) * 8 + j;
-            v = w[(size_t(co) * d.cin + ci) * kk + tap];
-          }
+          if (co < d.cout && in) v = w[(size_t(co) * d.cin + ci0 + j) * kk + tap];
           dst[j] = (_Float16)v;
         }
       }
@@ -183,8 +195,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   // Branch-free K loop: an out-of-image tap or padded K chunk loads a 16-byte zero line (address
   // select, never a value mask), so no load is conditional and hipcc places counted vmcnt waits;
   // D K-steps of fragments stay in flight (a ring of D register sets, unrolled: static indices).
-  // FAST (cin % 32 == 0): a K-step is 32 channels of ONE tap, so the (tap, step-in-tap) cursor is
-  // wave-uniform (scalar).  Otherwise each lane decodes its chunk c = 4s+grp with a magic divide.
+  // FAST (cin % 32 == 0): a K-step is 32 channels of ONE tap, ordered chunk-major (step =
+  // chunk * taps + tap, see conv_pack), so the (chunk, tap) cursor is wave-uniform (scalar).
+  // Otherwise each lane decodes its chunk c = 4s+grp with a magic divide.
   const h8* wfrag[RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
@@ -192,28 +205,30 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
   }
   const h8* zline = reinterpret_cast<const h8*>(g_zero_line);
-  const int spt = a.cpt >> 2;  // K-steps per tap (FAST)
-  int lt = 0, ls = 0;          // load cursor: tap, step within tap (FAST)
+  const int spt = a.cpt >> 2;  // 32-channel chunks (FAST)
+  int lt = 0, ls = 0;          // load cursor: tap, chunk (FAST)
   auto tap_off = [&](int t) -> int64_t {
     const int ky = (t * 11) >> 5;  // t / 3 for t < 9
     return KS == 1 ? 0 : (int64_t(ky) * a.Ws + (t - ky * 3)) * a.xcs;
   };
   auto load_b = [&](int s, h8 (&b)[RP]) {
     int t, ce;  // tap and element offset within the pixel's channels
+    bool tin;   // a real K-step (padded steps past the end load the zero line)
     if (FAST) {
       t = lt;
       ce = ls * 32 + grp * 8;
-      if (++ls == spt) {
-        ls = 0;
-        ++lt;
+      tin = ls < spt;
+      if (++lt == KS * KS) {
+        lt = 0;
+        ++ls;
       }
     } else {
       const unsigned c = unsigned(s * 4 + grp);
       t = a.cpt == 1 ? int(c) : int(__umulhi(c, a.cmagic));
       ce = (int(c) - t * a.cpt) * 8;
+      tin = t < KS * KS;
     }
     const int64_t toff = tap_off(t) + ce;
-    const bool tin = t < KS * KS;
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       const bool ok = tin && ((vmask[p] >> (t & 31)) & 1u);
@@ -378,6 +393,117 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
           if (OUT == OUT_ACCUM) t = (float)yo[j] + alpha * t;
           yo[j] = (_Float16)t;
         }
+      }
+    }
+  }
+}
+
+// ============================================================================ 3x3, LDS halo tiles
+// For cin % 32 == 0.  A block (4 waves) owns a 2-D output tile of TW = 16 columns x TH = 4*RP rows
+// of one image and RC*16 couts; wave w owns rows [w*RP, w*RP+RP) (one 16-pixel B fragment per row).
+// Per 32-channel chunk the input tile + halo ((TH-1)*S+3 x (TW-1)*S+3 pixels x 64 B) is staged in
+// LDS once with coalesced 16-byte loads, and all 9 taps read their B fragments from it (a wave
+// reads 16 consecutive pixels x 64 B = 1 KiB contiguous per fragment), instead of every tap
+// re-fetching the pixels from L2 as the implicit-GEMM kernel does.  A fragments: the same packed
+// layout (K-step = chunk * 9 + tap).  Per output element the K order (chunk-major, tap, channel)
+// is the implicit-GEMM kernel's, so both kernels give bitwise-identical results.
+template <int S, int RC, int RP>
+__global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
+  constexpr int TW = 16, TH = 4 * RP;
+  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;  // staged input rows / cols
+  __shared__ __attribute__((aligned(16))) h8 tile[RI * CI * 4];  // [row][col][4 x 8 channels]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int n = t / tiles_y;
+  const int ox0 = tx * TW, oy0 = ty * TH;
+  const int cot0 = blockIdx.y * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  const int spt = a.cin >> 5;  // 32-channel chunks = K-steps per tap
+  const h8* wfrag[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int ct = min(cot0 + r, cotiles - 1);
+    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
+  }
+  f4 acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  for (int cc = 0; cc < spt; ++cc) {
+    __syncthreads();  // previous chunk's reads done
+    for (int e = threadIdx.x; e < RI * CI * 4; e += 256) {
+      const int pc = e >> 2, q = e & 3;
+      const int r = pc / CI, c = pc - r * CI;
+      const int iy = iy0 + r, ix = ix0 + c;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws)
+        v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + cc * 32 + q * 8);
+      tile[e] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - ky * 3;
+      h8 af[RC], bf[RP];
+#pragma unroll
+      for (int r = 0; r < RC; ++r) af[r] = wfrag[r][(cc * 9 + tap) * 64];
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        const int ry = (wave * RP + p) * S + ky, cx = col * S + kx;
+        bf[p] = tile[(ry * CI + cx) * 4 + grp];
+      }
+#pragma unroll
+      for (int r = 0; r < RC; ++r)
+#pragma unroll
+        for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+    }
+  }
+  // epilogue: bias, SiLU, optional residual, fp16 NHWC store
+  const int ox = ox0 + col;
+  if (ox >= a.Wo) return;
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co0 = (cot0 + r) * 16 + grp * 4;
+    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int oy = oy0 + wave * RP + p;
+      if (oy >= a.Ho) continue;
+      const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float tt = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(tt) : tt;
+      }
+      _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
+      if (a.res) {
+        const _Float16* ro = a.res + pix * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          const h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] += (float)ro[j];
+        }
+      }
+      if (a.vec_ok && co0 + 3 < a.cout) {
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) yo[j] = (_Float16)v[j];
       }
     }
   }
@@ -968,7 +1094,45 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int rp : {1, 2, 4})
       if (n < cap) out[n++] = rc | (rp << 4);
   }
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel, coded 0x100 | rc | rp << 4
+    for (int rc : {1, 2, 4}) {
+      if (rc > 1 && (rc >> 1) >= cotiles) continue;
+      for (int rp : {1, 2, 4})
+        if (n < cap) out[n++] = 0x100 | rc | (rp << 4);
+    }
   return n;
+}
+
+template <int S, int RC>
+static void launch_tile3_rc(const ConvArgs& a, int rp, dim3 grid, hipStream_t s) {
+  if (rp == 1)
+    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 1>), grid, dim3(256), 0, s, a);
+  else if (rp == 2)
+    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 2>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 4>), grid, dim3(256), 0, s, a);
+}
+
+template <int S>
+static void launch_tile3_s(const ConvArgs& a, int rc, int rp, dim3 grid, hipStream_t s) {
+  if (rc == 1)
+    launch_tile3_rc<S, 1>(a, rp, grid, s);
+  else if (rc == 2)
+    launch_tile3_rc<S, 2>(a, rp, grid, s);
+  else
+    launch_tile3_rc<S, 4>(a, rp, grid, s);
+}
+
+static int launch_tile3(const ConvArgs& a, int rc, int rp, int stride, int n, hipStream_t s) {
+  const int th = 4 * rp;
+  const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
+  FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
+  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + rc - 1) / rc));
+  if (stride == 1)
+    launch_tile3_s<1>(a, rc, rp, grid, s);
+  else
+    launch_tile3_s<2>(a, rc, rp, grid, s);
+  return launch_status("conv3x3_tile_kernel");
 }
 
 int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
@@ -1116,7 +1280,16 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_hw = Ho * Wo;
   a.det_w = Wo;
   a.det_stride = det ? det->stride : 0.f;
+  const bool fast = d.cin % 32 == 0;
   int rc, rp;
+  if (tile >= 0x100) {  // LDS halo-tile 3x3 kernel
+    rc = tile & 15;
+    rp = (tile >> 4) & 15;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (rc == 1 || rc == 2 || rc == 4) &&
+                  (rp == 1 || rp == 2 || rp == 4),
+              "conv: bad LDS-tile hint");
+    return launch_tile3(a, rc, rp, d.stride, x.n, s);
+  }
   if (tile >= 0) {
     rc = tile & 15;
     rp = tile >> 4;
@@ -1126,7 +1299,6 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   }
   if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
   if (d.k == 3) FCE_CHECK(d.up == 0 && out_kind == OUT_F16, "conv 3x3: plain fp16 store, no fused upsampling");
-  const bool fast = d.cin % 32 == 0;
   if (d.k == 1)
     launch_dense_rc<1>(a, out_kind, fast, rc, rp, s);
   else

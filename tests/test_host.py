@@ -104,14 +104,19 @@ def _pack_ref(w, cin, cout, k):
     for ct in range(cot):
         for s in range(nsteps):
             for l in range(64):
-                co, c = ct * 16 + (l & 15), s * 4 + (l >> 4)
-                if co < cout and c < nchunk:
-                    tap, ci = c // cpt, (c % cpt) * 8
+                co = ct * 16 + (l & 15)
+                if cin % 32 == 0:  # chunk-major: step = 32-channel chunk * k*k + tap
+                    tap, ci = s % (k * k), (s // (k * k)) * 32 + (l >> 4) * 8
+                    ok = True
+                else:  # 8-channel chunks c = 4s + lane/16, tap-major
+                    c = s * 4 + (l >> 4)
+                    tap, ci, ok = c // cpt, (c % cpt) * 8, c < nchunk
+                if co < cout and ok:
                     out[ct, s, l] = w[co, ci:ci + 8, tap // k, tap % k]
     return out
 
 
-@pytest.mark.parametrize("cin,cout,k", [(8, 16, 3), (16, 8, 3), (32, 40, 1), (64, 80, 3), (24, 24, 1)])
+@pytest.mark.parametrize("cin,cout,k", [(8, 16, 3), (16, 8, 3), (32, 40, 1), (64, 80, 3), (24, 24, 1), (96, 32, 3)])
 def test_dense_weight_packing(cin, cout, k):
     w = np.random.default_rng(0).standard_normal((cout, cin, k, k)).astype(np.float32)
     d = N.ConvDesc(cin, cout, k, 1, 1, 1, 0, 0, None, 0, 0)
