@@ -119,7 +119,7 @@ _SIGS = {
     "fce_net_arena_bytes": (_SZ, [_P]),
     "fce_net_num_anchors": (_I, [_P]),
     "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),
-    "fce_net_profile": (_I, [_P, _PT, _P, _P, _I, _P]),
+    "fce_net_profile": (_I, [_P, _PT, _P, _P, _P, _I, _P]),
     "fce_net_num_ops": (_I, [_P]),
     "fce_net_op_info": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fce_net_buffer": (_I, [_P, _I, _PT]),

@@ -42,6 +42,8 @@ int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_
         void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
 
 static thread_local std::string g_err;
+static thread_local LaunchProbe* g_probe = nullptr;
+LaunchProbe*& probe_slot() { return g_probe; }
 void set_error(const std::string& m) { g_err = m; }
 int fail(int code, const std::string& m) {
   g_err = m;
@@ -830,26 +832,52 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
   })
 }
 
-int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int cap, void* stream) {
+int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int* launches, int cap,
+                    void* stream) {
   FCE_CHECK(net && pred && ms, "fce_net_profile: null argument");
   int st = check_input(net, input);
   if (st) return st;
   hipStream_t s = S(stream);
   FCE_GUARD({
+    // every kernel of every op carries its own (start, stop) event pair (hipExtLaunchKernelGGL): an
+    // op's time is the sum of its kernels' execution intervals, the quantity rocprofv3 reports
+    constexpr int kPerOp = 16;
     const int nops = int(net->ops.size());
-    std::vector<hipEvent_t> ev(nops + 1);
-    for (auto& e : ev) FCE_HIP_CHECK(hipEventCreate(&e));
-    FCE_HIP_CHECK(hipEventRecord(ev[0], s));
-    for (int i = 0; i < nops; ++i) {
+    std::vector<hipEvent_t> ev(size_t(nops) * kPerOp * 2, nullptr);
+    std::vector<int> used(nops, 0);
+    auto destroy = [&]() {
+      for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    };
+    for (auto& e : ev) {
+      if (hipEventCreate(&e) != hipSuccess) {
+        destroy();
+        return fail(FCE_ERR_HIP, "fce_net_profile: hipEventCreate failed");
+      }
+    }
+    for (int i = 0; i < nops && !st; ++i) {
+      LaunchProbe probe{ev.data() + size_t(i) * kPerOp * 2, kPerOp, 0};
+      g_probe = &probe;
       st = run_op(net, net->ops[i], *input, pred, s);
-      if (st) break;
-      FCE_HIP_CHECK(hipEventRecord(ev[i + 1], s));
+      g_probe = nullptr;
+      used[i] = probe.n;
     }
-    if (!st) {
-      FCE_HIP_CHECK(hipEventSynchronize(ev[nops]));
-      for (int i = 0; i < nops && i < cap; ++i) FCE_HIP_CHECK(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+    if (!st && hipStreamSynchronize(s) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_profile: sync failed");
+    for (int i = 0; i < nops && i < cap && !st; ++i) {
+      float tot = 0.f;
+      for (int k = 0; k < used[i]; ++k) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, ev[(size_t(i) * kPerOp + k) * 2], ev[(size_t(i) * kPerOp + k) * 2 + 1]) !=
+            hipSuccess) {
+          st = fail(FCE_ERR_HIP, "fce_net_profile: hipEventElapsedTime failed");
+          break;
+        }
+        tot += t;
+      }
+      ms[i] = tot;
+      if (launches) launches[i] = used[i];
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
+    destroy();
     return st;
   })
 }

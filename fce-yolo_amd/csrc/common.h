@@ -1,7 +1,8 @@
 // Shared helpers for the gfx950 kernels and the C-ABI glue.
 #pragma once
-#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -39,6 +40,27 @@ inline int launch_status(const char* what) {
   if (e != hipSuccess) return fail(FCE_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   return FCE_OK;
 }
+
+// ---------------------------------------------------------------- per-kernel timing probe
+// While fce_net_profile runs an op, g_probe points at a pool of timing events and every launch goes
+// through hipExtLaunchKernelGGL with a (start, stop) pair attached to its own dispatch packet, so the
+// measured interval is exactly the kernel's execution (no event packets between kernels).
+struct LaunchProbe {
+  hipEvent_t* ev;  // 2 * cap events
+  int cap, n;      // pairs available / used
+};
+LaunchProbe*& probe_slot();  // thread-local slot (api.hip)
+
+#define FCE_LAUNCH(K, G, B, SH, S, ...)                                                            \
+  do {                                                                                             \
+    ::fce::LaunchProbe* _p = ::fce::probe_slot();                                                       \
+    if (_p && _p->n < _p->cap) {                                                                   \
+      hipExtLaunchKernelGGL(K, G, B, SH, S, _p->ev[2 * _p->n], _p->ev[2 * _p->n + 1], 0, __VA_ARGS__); \
+      ++_p->n;                                                                                     \
+    } else {                                                                                       \
+      hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                             \
+    }                                                                                              \
+  } while (0)
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -737,9 +737,9 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
       if (lds > 64 * 1024) continue;
       dim3 g((x.c + CS - 1) / CS, y.n * Ho);
       if (stride == 1)
-        hipLaunchKernelGGL((dwconv_rows_kernel<1>), g, dim3(256), lds, s, a, CS);
+        FCE_LAUNCH((dwconv_rows_kernel<1>), g, dim3(256), lds, s, a, CS);
       else
-        hipLaunchKernelGGL((dwconv_rows_kernel<2>), g, dim3(256), lds, s, a, CS);
+        FCE_LAUNCH((dwconv_rows_kernel<2>), g, dim3(256), lds, s, a, CS);
       return launch_status("dwconv_rows_kernel");
     }
   }
@@ -747,17 +747,17 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
     const int cg = x.c / 8;
     const int threads = (256 / cg) * cg;
     if (stride == 1)
-      hipLaunchKernelGGL((dwconv_lanes_kernel<1>), dim3(y.n * Ho), dim3(threads), 0, s, a);
+      FCE_LAUNCH((dwconv_lanes_kernel<1>), dim3(y.n * Ho), dim3(threads), 0, s, a);
     else
-      hipLaunchKernelGGL((dwconv_lanes_kernel<2>), dim3(y.n * Ho), dim3(threads), 0, s, a);
+      FCE_LAUNCH((dwconv_lanes_kernel<2>), dim3(y.n * Ho), dim3(threads), 0, s, a);
     return launch_status("dwconv_lanes_kernel");
   }
   constexpr int PX = 4;
   dim3 grid(((Wo + PX - 1) / PX * (x.c / 8) + 255) / 256, y.n * Ho);
   if (stride == 1)
-    hipLaunchKernelGGL((dwconv_kernel<1, PX>), grid, dim3(256), 0, s, a);
+    FCE_LAUNCH((dwconv_kernel<1, PX>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((dwconv_kernel<2, PX>), grid, dim3(256), 0, s, a);
+    FCE_LAUNCH((dwconv_kernel<2, PX>), grid, dim3(256), 0, s, a);
   return launch_status("dwconv_kernel");
 }
 
@@ -995,7 +995,7 @@ static int grid_cap(int64_t blocks) { return int(blocks < 65535 * 16 ? blocks : 
 
 template <int KS, int RC, int RP>
 static void launch_dense(const ConvArgs& a, int out_kind, bool fast, dim3 grid, hipStream_t s) {
-#define CONV_L(O, F) hipLaunchKernelGGL((conv_mfma_kernel<KS, RC, RP, O, F>), grid, dim3(256), 0, s, a)
+#define CONV_L(O, F) FCE_LAUNCH((conv_mfma_kernel<KS, RC, RP, O, F>), grid, dim3(256), 0, s, a)
 #define CONV_O(O)  \
   if (fast)        \
     CONV_L(O, true); \
@@ -1106,11 +1106,11 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
 template <int S, int RC>
 static void launch_tile3_rc(const ConvArgs& a, int rp, dim3 grid, hipStream_t s) {
   if (rp == 1)
-    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 1>), grid, dim3(256), 0, s, a);
+    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 1>), grid, dim3(256), 0, s, a);
   else if (rp == 2)
-    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 2>), grid, dim3(256), 0, s, a);
+    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 2>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((conv3x3_tile_kernel<S, RC, 4>), grid, dim3(256), 0, s, a);
+    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 4>), grid, dim3(256), 0, s, a);
 }
 
 template <int S>
@@ -1164,7 +1164,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
       FCE_CHECK(threads < (int64_t(1) << 31), "stem conv: input too large");
       const dim3 grid(unsigned((threads + 255) / 256));
 #define STEM2_LAUNCH(CT, P, T)                                                                       \
-  hipLaunchKernelGGL((stem_s2_kernel<CT, P, T>), grid, dim3(256), shm + size_t(256) * P * CT * 2, s, a)
+  FCE_LAUNCH((stem_s2_kernel<CT, P, T>), grid, dim3(256), shm + size_t(256) * P * CT * 2, s, a)
 #define STEM2_DT(CT, P)                  \
   do {                                   \
     if (x.dtype == FCE_F16)              \
@@ -1186,7 +1186,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
 #undef STEM2_LAUNCH
       return launch_status("stem_s2_kernel");
     }
-#define STEM_LAUNCH(CT, T) hipLaunchKernelGGL((stem_kernel<CT, T>), dim3(blocks), dim3(256), shm, s, a)
+#define STEM_LAUNCH(CT, T) FCE_LAUNCH((stem_kernel<CT, T>), dim3(blocks), dim3(256), shm, s, a)
 #define STEM_DT(CT)                      \
   do {                                   \
     if (x.dtype == FCE_F16)              \

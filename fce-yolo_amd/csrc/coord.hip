@@ -293,7 +293,7 @@ static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
   for (int i = 0; i < nj; ++i) maxKM = std::max(maxKM, jobs[i].K * jobs[i].M);
   const int wlds = (size_t(TP) * maxK + maxKM) * sizeof(float) <= 64 * 1024;
   dim3 grid((maxL + TP - 1) / TP, nj, N);
-  hipLaunchKernelGGL(coord_proj_kernel, grid, dim3(256), (size_t(TP) * maxK + (wlds ? maxKM : 0)) * sizeof(float), s,
+  FCE_LAUNCH(coord_proj_kernel, grid, dim3(256), (size_t(TP) * maxK + (wlds ? maxKM : 0)) * sizeof(float), s,
                      pa, TP, wlds);
   return launch_status("coord_proj_kernel");
 }
@@ -325,7 +325,7 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
                                                     hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                                     int(kMaxLds)) == hipSuccess;                        \
     if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord attention: cannot opt in to >64 KiB LDS"); \
-    hipLaunchKernelGGL(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a);                            \
+    FCE_LAUNCH(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a);                            \
     break;                                                                                              \
   }
     ATT(1) ATT(2) ATT(3) ATT(4) ATT(5) ATT(6) ATT(7) ATT(8) ATT(10) ATT(12) ATT(16) ATT(20) ATT(24) ATT(32)
@@ -355,9 +355,9 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   ws_layout(d, N, H, W, &w, static_cast<float*>(ws));
   const _Float16* xp = static_cast<const _Float16*>(x.data) + x.coff;
   const int C = d.inp, mid = d.mid;
-  hipLaunchKernelGGL(pool_rows_kernel, dim3(H, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh);
+  FCE_LAUNCH(pool_rows_kernel, dim3(H, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh);
   const int XW = 256 / (C / 8);
-  hipLaunchKernelGGL(pool_cols_kernel, dim3((W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xw);
+  FCE_LAUNCH(pool_cols_kernel, dim3((W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xw);
   int st = launch_status("coord pooling");
   if (st) return st;
   if (kind == 0) {  // BiCoordCrossAtt
@@ -405,13 +405,13 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   FCE_CHECK(int64_t(N) * H < 65536 * 1024, "coord attention: too many rows");
   const dim3 grid((W * (d.oup / 8) + 255) / 256, N * H);
   if (kind == 0)
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_BICOORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
+    FCE_LAUNCH(gate_apply_kernel<GATE_BICOORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
                        d.oup, w.g1, w.g2);
   else if (kind == 1)
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_COORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+    FCE_LAUNCH(gate_apply_kernel<GATE_COORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
                        w.g1, w.g2);
   else
-    hipLaunchKernelGGL(gate_apply_kernel<GATE_ROW>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+    FCE_LAUNCH(gate_apply_kernel<GATE_ROW>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
                        w.g1, w.g2);
   return launch_status("gate_apply_kernel");
 }

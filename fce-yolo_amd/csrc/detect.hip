@@ -97,7 +97,7 @@ int detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const fl
   a.A = A;
   const int64_t total = int64_t(a.N) * A;
   if (total == 0) return FCE_OK;
-  hipLaunchKernelGGL(detect_decode_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256),
+  FCE_LAUNCH(detect_decode_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256),
                      0, s, a);
   return launch_status("detect_decode_kernel");
 }

@@ -568,9 +568,9 @@ int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_
   const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
   const int stop = stop_env ? atoi(stop_env) : 0;
   if (A > 0)
-    hipLaunchKernelGGL(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
+    FCE_LAUNCH(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);
-  hipLaunchKernelGGL(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, nc, A, conf, iou, max_det, max_nms, max_wh,
+  FCE_LAUNCH(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, nc, A, conf, iou, max_det, max_nms, max_wh,
                      static_cast<char*>(ws), per, dets, keep, counts, stop);
   return launch_status("nms_kernel");
 }

@@ -151,11 +151,11 @@ int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y
   if (total == 0) return FCE_OK;
   const size_t lds = size_t(4) * x.h * x.w * sizeof(h8);
   if (lds <= 64 * 1024 && int64_t(x.n) * (x.c / 8) < (int64_t(1) << 31)) {  // H*W <= 1024 (imgsz <= 1024)
-    hipLaunchKernelGGL(maxpool_chain_lds_kernel, dim3(x.n * (x.c / 8)), dim3(256), lds, s, a);
+    FCE_LAUNCH(maxpool_chain_lds_kernel, dim3(x.n * (x.c / 8)), dim3(256), lds, s, a);
     return launch_status("maxpool_chain_lds_kernel");
   }
   int blocks = int(std::min<int64_t>((total + 255) / 256, 65535 * 8));
-  hipLaunchKernelGGL(maxpool_chain_kernel, dim3(blocks), dim3(256), 0, s, a);
+  FCE_LAUNCH(maxpool_chain_kernel, dim3(blocks), dim3(256), 0, s, a);
   return launch_status("maxpool_chain_kernel");
 }
 
@@ -200,7 +200,7 @@ int weighted_add(const fce_tensor& x, int up, const float* fw, int fn, int fi, i
              static_cast<_Float16*>(y.data) + y.coff, y.cstride, y.n, y.h, y.w, y.c, fw, fn, fi, accumulate};
   const int64_t total = int64_t(y.n) * y.h * y.w * (y.c / 8);
   if (total == 0) return FCE_OK;
-  hipLaunchKernelGGL(weighted_add_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256),
+  FCE_LAUNCH(weighted_add_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256),
                      0, s, a);
   return launch_status("weighted_add_kernel");
 }
@@ -258,7 +258,7 @@ int copy(const fce_tensor& src, const fce_tensor& dst, hipStream_t s) {
   if (total == 0) return FCE_OK;
   CopyArgs a{src.data, src.dtype, src.layout, src.cstride, src.coff, dst.data, dst.dtype,
              dst.layout, dst.cstride, dst.coff, src.n, src.c, src.h, src.w};
-  hipLaunchKernelGGL(copy_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256), 0, s, a);
+  FCE_LAUNCH(copy_kernel, dim3(int(std::min<int64_t>((total + 255) / 256, 65535 * 8))), dim3(256), 0, s, a);
   return launch_status("copy_kernel");
 }
 

@@ -151,7 +151,7 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
   }
   dim3 grid((N + 63) / 64, heads, qkv.n);
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)key_dim);
-  hipLaunchKernelGGL((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
+  FCE_LAUNCH((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
                      static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
                      static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
   return launch_status("psa_attention_mfma_kernel");

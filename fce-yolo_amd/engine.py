@@ -67,13 +67,17 @@ class Engine:
         N.call("fce_net_forward", self.be.net, C.byref(self._in(x)), out.data_ptr(), int(bool(g)), stream)
         return out
 
-    def profile(self, x: torch.Tensor):
-        """Eager run with a hipEvent pair around every op: [(name, ms, bytes, flops)]."""
+    def profile(self, x: torch.Tensor, launches: bool = False):
+        """Eager run, every kernel timed by its own dispatch-attached event pair:
+        [(name, bytes, flops, ms)] per op (+ kernel count per op when `launches`)."""
         n = N.lib().fce_net_num_ops(self.be.net)
         ms = (C.c_float * n)()
+        nl = (C.c_int * n)()
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        N.call("fce_net_profile", self.be.net, C.byref(self._in(x)), self.pred.data_ptr(), C.cast(ms, C.c_void_p), n,
-               stream)
+        N.call("fce_net_profile", self.be.net, C.byref(self._in(x)), self.pred.data_ptr(), C.cast(ms, C.c_void_p),
+               C.cast(nl, C.c_void_p), n, stream)
+        if launches:
+            return [(*self.op_info(i), float(ms[i]), int(nl[i])) for i in range(n)]
         return [(*self.op_info(i), float(ms[i])) for i in range(n)]
 
     def op_info(self, i: int):

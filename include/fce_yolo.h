@@ -196,8 +196,11 @@ int fce_net_num_anchors(const fce_net* net);
  * graph=1 captures the whole forward into a hipGraph on first use for these pointers and
  * replays it afterwards (re-captured if the pointers change). */
 int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int graph, void* stream);
-/* Eager run recording a hipEvent pair around every op: ms[i] per op (cap entries). */
-int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int cap, void* stream);
+/* Eager run in which every kernel is launched with its own (start, stop) event pair
+ * (hipExtLaunchKernelGGL): ms[i] = summed kernel execution time of op i, launches[i] (nullable) = its
+ * kernel count (cap entries each). */
+int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int* launches, int cap,
+                    void* stream);
 int fce_net_num_ops(const fce_net* net);
 /* name (kernel family), algorithmic bytes and flops of op i at the planned size */
 int fce_net_op_info(const fce_net* net, int i, char* name, int name_cap, double* bytes, double* flops);

@@ -22,6 +22,8 @@ x = torch.rand(B, 3, 640, 640, generator=torch.Generator().manual_seed(1000)).ha
 eng = Engine(model, B, 640, dev)
 pred = eng(x).clone()
 nms = NMS(B, eng.anchors, eng.nc, dev)
+ncand = (pred[:, 4:].amax(1) > 0.25).sum(1)
+print("candidates per image: min", int(ncand.min()), "max", int(ncand.max()), "of", eng.anchors, flush=True)
 for stop in ("1", "2", "3", "0"):
     os.environ["FCE_NMS_STOP"] = stop
     for _ in range(3):
