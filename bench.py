@@ -4,8 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-A step = one hipGraph replay of the whole forward over a resident synthetic batch
-(torch.rand(B,3,S,S) fp16, seeded per rank) + the device NMS of that batch.  Weights are the
+A step = the whole forward (direct launches; --graph 1 for hipGraph replay) over a resident synthetic
+batch (torch.rand(B,3,S,S) fp16, seeded per rank) + the device NMS of that batch.  By default the NMS of
+batch i runs on a side stream under the forward of batch i+1 (engine.Pipeline, double-buffered pred);
+--sequential runs them back to back.  Weights are the
 portable seeded weights of the named architecture (no checkpoints offline), broadcast from rank 0
 over RCCL.  Each rank owns its own batch shard (contiguous, reference ContiguousDistributedSampler
 rule); there is no data-path collective, so scaling is weak.  Prints ONE JSON line on rank 0.
@@ -30,7 +32,7 @@ import fce_pkg  # noqa: E402
 
 fce_pkg.load()
 from fce_yolo_amd.dist import broadcast_module  # noqa: E402
-from fce_yolo_amd.engine import NMS, Engine  # noqa: E402
+from fce_yolo_amd.engine import NMS, Engine, Pipeline  # noqa: E402
 from fce_yolo_amd.parser import DetectionModel, load_cfg  # noqa: E402
 from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
 
@@ -65,6 +67,7 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
+    ap.add_argument("--sequential", action="store_true", help="forward then NMS on one stream (no overlap)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay a captured hipGraph; 0: direct launches "
                     "(measured faster on ROCm 7.2, DESIGN.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
@@ -137,16 +140,20 @@ def main():
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
     eng = Engine(model, B, S, dev, graph=bool(a.graph))
     nms = NMS(B, eng.anchors, eng.nc, dev)
+    pipe = Pipeline(eng, depth=2)
 
     def step():
-        pred = eng(x)
-        if not a.no_nms:
-            nms(pred)
+        if a.no_nms:
+            eng(x)
+        elif a.sequential:
+            nms(eng(x))
+        else:  # forward of this batch overlaps the NMS of the previous one (engine.Pipeline)
+            pipe.submit(x)
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize()  # device-wide: includes the NMS side stream
 
     for _ in range(a.warmup):
         step()

@@ -30,7 +30,14 @@ static constexpr int RADIX_CAP = 8192;   // LDS radix sort capacity (16 waves x 
 static constexpr int REMOVED_CAP = 32768;
 static constexpr int KEPT_CAP = 1024;    // kept boxes held in LDS by the tiled path
 static constexpr int TILE = 64;
-static constexpr int WIN = NMS_THREADS;  // frontier extension step
+static constexpr int WIN = 256;  // frontier extension step
+// small-set fast path: <= HEAD_CAP candidates sorted in LDS (1024 or 2048 slots instead of 8192).  Pool
+// layout of that sort:
+//   sort | keysA 8K | keysB 8K | valsA 4K | valsB 4K | wcnt (histogram) 16K |
+// the greedy then uses the full layout's regions below valsA (removed | kept box | area | cand).
+static constexpr int HEAD_CAP = 2048;
+static constexpr int H_OFF_KA = 0, H_OFF_KB = 8 * 1024, H_OFF_VA = 16 * 1024, H_OFF_VB = 20 * 1024,
+                     H_OFF_WC = 24 * 1024;
 
 // LDS pool (bytes): sort phase  | keysA 32K | keysB 32K | valsA 16K | valsB 16K | wcnt 16K |
 //                   greedy      | removed   | kept box+area | spos (= sorted valsA) |
@@ -129,10 +136,11 @@ __device__ void bitonic_desc(uint64_t* k, int n2) {
   }
 }
 
-// Stable LSD radix sort of RADIX_CAP (key, index) pairs by ascending key, in LDS.  Wave w owns
-// positions [512w, 512w+512) in lane-striped order (item j of lane l = 512w + 64j + l), so the
+// Stable LSD radix sort of 1024 * IPL (key, index) pairs by ascending key, in LDS.  Wave w owns
+// positions [64 IPL w, 64 IPL (w+1)) in lane-striped order (item j of lane l = 64 IPL w + 64j + l), so the
 // ballot-matched running rank of a digit inside the wave is its stable rank; per-(digit, wave)
 // counts are then scanned digit-major for the global offsets.
+template <int IPL>
 __device__ void radix_sort_lds(uint32_t* kA, uint32_t* kB, uint16_t* vA, uint16_t* vB, int* wcnt, int* wsum) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -144,19 +152,19 @@ __device__ void radix_sort_lds(uint32_t* kA, uint32_t* kB, uint16_t* vA, uint16_
     const int shift = 8 * pass;
     for (int e = threadIdx.x; e < NWAVES * 256; e += NMS_THREADS) wcnt[e] = 0;
     __syncthreads();
-    uint32_t k[8];
-    uint16_t v[8];
-    int d[8], rank[8];
+    uint32_t k[IPL];
+    uint16_t v[IPL];
+    int d[IPL], rank[IPL];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int idx = 512 * wv + 64 * j + lane;
+    for (int j = 0; j < IPL; ++j) {
+      const int idx = 64 * IPL * wv + 64 * j + lane;
       k[j] = ks[idx];
       v[j] = vs[idx];
       d[j] = int((k[j] >> shift) & 255u);
     }
     int* wc = wcnt + wv * 256;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < IPL; ++j) {
       uint64_t peer = ~0ull;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
@@ -199,7 +207,7 @@ __device__ void radix_sort_lds(uint32_t* kA, uint32_t* kB, uint16_t* vA, uint16_
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < IPL; ++j) {
       const int pos = wc[d[j]] + rank[j];
       kd[pos] = k[j];
       vd[pos] = v[j];
@@ -316,43 +324,6 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
   degenerate = __syncthreads_or(degenerate);
   if (stop == 1) return;  // phase timing (FCE_NMS_STOP, diagnostics only)
 
-  // ---- 2. order (score desc, candidate position asc)
-  const bool lds_sorted = ncand <= RADIX_CAP;
-  const uint16_t* spos16 = reinterpret_cast<const uint16_t*>(pool + 0);
-  if (lds_sorted) {
-    uint32_t* kA = reinterpret_cast<uint32_t*>(pool);
-    uint16_t* vA = reinterpret_cast<uint16_t*>(pool + OFF_VA);
-    for (int i = threadIdx.x; i < RADIX_CAP; i += NMS_THREADS) {
-      kA[i] = i < ncand ? ~__float_as_uint(w.cscore[i]) : 0xFFFFFFFFu;  // scores > conf >= 0
-      vA[i] = uint16_t(i);
-    }
-    __syncthreads();
-    radix_sort_lds(kA, reinterpret_cast<uint32_t*>(pool + OFF_KB), vA, reinterpret_cast<uint16_t*>(pool + OFF_VB),
-                   reinterpret_cast<int*>(pool + OFF_WC), wsum);
-    spos16 = vA;
-  } else {
-    const int n2 = next_pow2_dev(ncand);
-    for (int i = threadIdx.x; i < n2; i += NMS_THREADS) {
-      uint64_t k = 0;
-      if (i < ncand) k = (uint64_t(__float_as_uint(w.cscore[i])) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(i));
-      w.keys[i] = k;
-    }
-    __syncthreads();
-    bitonic_desc(w.keys, n2);
-    for (int i = threadIdx.x; i < min(ncand, max_nms); i += NMS_THREADS)
-      w.spos[i] = int(0xFFFFFFFFu - uint32_t(w.keys[i] & 0xFFFFFFFFull));
-    __syncthreads();
-  }
-  const int M = min(ncand, max_nms);
-  auto sp = [&](int i) -> int { return lds_sorted ? int(spos16[i]) : w.spos[i]; };
-  uint8_t* lremoved = reinterpret_cast<uint8_t*>(pool);  // sort keys are dead from here
-  float4* kbox = reinterpret_cast<float4*>(pool + OFF_KBOX);
-  float* karea = reinterpret_cast<float*>(pool + OFF_KAREA);
-  int* kidx = reinterpret_cast<int*>(pool + OFF_KIDX);  // kept slot -> candidate (dets written at the end)
-  if (threadIdx.x == 0) s_kept = 0;
-  __syncthreads();
-  if (stop == 2) return;
-
   auto emit_det = [&](int c, int slot) {
     const int a = w.cidx[c];
     const float cx = P[a], cy = P[int64_t(1) * A + a];
@@ -366,40 +337,163 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
     d[5] = (float)w.ccls[c];
     keep[int64_t(n) * max_det + slot] = a;
   };
+  const int M = min(ncand, max_nms);
+  const bool tiled = !degenerate && max_det <= KEPT_CAP;
 
-  // Lanes' candidates (bj, aj) vs kept boxes [kf, kl): the kept boxes are staged 64 at a time in
-  // lane registers and broadcast with v_readlane, so the inner loop is VALU only (no LDS latency).
-  auto kept_suppress = [&](float4 bj, float aj, bool act, int kf, int kl) -> bool {
-    bool rem = false;
-    for (int c0 = kf; c0 < kl; c0 += 64) {
-      const int m = min(64, kl - c0);
-      float4 kb = make_float4(0.f, 0.f, 0.f, 0.f);
-      float ka = 0.f;
-      if (lane < m) {
-        kb = kbox[c0 + lane];
-        ka = karea[c0 + lane];
+  // ---- 2h. small candidate sets (<= HEAD_CAP, the usual case for a trained model) are sorted in 1024 or
+  // 2048 LDS slots instead of RADIX_CAP (FCE_NMS_STOP=3, diagnostics: always the full sort)
+  int hn = 0;
+  bool head = false;
+  if (tiled && stop != 3) {
+    hn = ncand;
+    head = hn <= HEAD_CAP && hn > 0;
+    if (head) {
+      uint32_t* kA = reinterpret_cast<uint32_t*>(pool + H_OFF_KA);
+      uint16_t* vA = reinterpret_cast<uint16_t*>(pool + H_OFF_VA);
+      const int cap = hn <= 1024 ? 1024 : 2048;
+      for (int i = threadIdx.x; i < cap; i += NMS_THREADS) {
+        kA[i] = i < hn ? ~__float_as_uint(w.cscore[i]) : 0xFFFFFFFFu;  // scores > conf >= 0
+        vA[i] = uint16_t(i);
       }
-      auto rl = [](float x, int t) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), t)); };
-      for (int t = 0; t < m; ++t) {
-        const float4 b = make_float4(rl(kb.x, t), rl(kb.y, t), rl(kb.z, t), rl(kb.w, t));
-        const float a = rl(ka, t);
-        if (act && !rem) rem = suppresses(b, a, bj, aj, iou_thres);
+      __syncthreads();
+      if (cap == 1024)
+        radix_sort_lds<1>(kA, reinterpret_cast<uint32_t*>(pool + H_OFF_KB), vA,
+                          reinterpret_cast<uint16_t*>(pool + H_OFF_VB), reinterpret_cast<int*>(pool + H_OFF_WC), wsum);
+      else
+        radix_sort_lds<2>(kA, reinterpret_cast<uint32_t*>(pool + H_OFF_KB), vA,
+                          reinterpret_cast<uint16_t*>(pool + H_OFF_VB), reinterpret_cast<int*>(pool + H_OFF_WC), wsum);
+      __syncthreads();
+    }
+  }
+  if (stop == 2) return;
+
+  for (int attempt = head ? 0 : 1; attempt < 2; ++attempt) {  // one pass: the small or the full sort
+    const bool H = attempt == 0;
+    int Mg = M;  // sorted positions this attempt covers
+    bool lds_sorted = true;
+    const uint16_t* spos16 = reinterpret_cast<const uint16_t*>(pool + (H ? H_OFF_VA : OFF_VA));
+    if (H) {
+      Mg = min(hn, M);
+    } else {
+      // ---- 2f. order the full candidate list (score desc, candidate position asc)
+      lds_sorted = ncand <= RADIX_CAP;
+      if (lds_sorted) {
+        uint32_t* kA = reinterpret_cast<uint32_t*>(pool);
+        uint16_t* vA = reinterpret_cast<uint16_t*>(pool + OFF_VA);
+        for (int i = threadIdx.x; i < RADIX_CAP; i += NMS_THREADS) {
+          kA[i] = i < ncand ? ~__float_as_uint(w.cscore[i]) : 0xFFFFFFFFu;  // scores > conf >= 0
+          vA[i] = uint16_t(i);
+        }
+        __syncthreads();
+        radix_sort_lds<8>(kA, reinterpret_cast<uint32_t*>(pool + OFF_KB), vA,
+                          reinterpret_cast<uint16_t*>(pool + OFF_VB), reinterpret_cast<int*>(pool + OFF_WC), wsum);
+      } else {
+        const int n2 = next_pow2_dev(ncand);
+        for (int i = threadIdx.x; i < n2; i += NMS_THREADS) {
+          uint64_t k = 0;
+          if (i < ncand) k = (uint64_t(__float_as_uint(w.cscore[i])) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(i));
+          w.keys[i] = k;
+        }
+        __syncthreads();
+        bitonic_desc(w.keys, n2);
+        for (int i = threadIdx.x; i < M; i += NMS_THREADS)
+          w.spos[i] = int(0xFFFFFFFFu - uint32_t(w.keys[i] & 0xFFFFFFFFull));
+        __syncthreads();
       }
     }
-    return rem;
-  };
+    auto sp = [&](int i) -> int { return lds_sorted ? int(spos16[i]) : w.spos[i]; };
+    // greedy state over the dead sort keys (the sorted positions, spos16, stay live in either layout)
+    uint8_t* lremoved = reinterpret_cast<uint8_t*>(pool);
+    float4* kbox = reinterpret_cast<float4*>(pool + OFF_KBOX);
+    float* karea = reinterpret_cast<float*>(pool + OFF_KAREA);
+    int* kidx = reinterpret_cast<int*>(pool + OFF_KIDX);  // kept slot -> candidate
+    if (threadIdx.x == 0) s_kept = 0;
+    __syncthreads();
 
-  if (!degenerate && max_det <= KEPT_CAP) {
+    if (!tiled) {
+      // ---- 3b. literal per-box greedy (TorchNMS.nms with its early exit) for degenerate boxes
+      for (int i = threadIdx.x; i < M; i += NMS_THREADS) lremoved[i] = 0;
+      __syncthreads();
+      int kept = 0;
+      for (int i = 0; i < M && kept < max_det; ++i) {
+        if (lremoved[i]) continue;
+        const int ci = sp(i);
+        if (threadIdx.x == 0) emit_det(ci, kept);
+        ++kept;
+        if (kept >= max_det) break;
+        const float4 bi = w.cbox[ci];
+        const float ai = w.carea[ci];
+        int any = 0;
+        for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
+          if (lremoved[j]) continue;
+          const int cj = sp(j);
+          float inter;
+          iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
+          any |= inter != 0.0f;
+        }
+        any = __syncthreads_or(any);
+        if (any) {
+          for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
+            if (lremoved[j]) continue;
+            const int cj = sp(j);
+            float inter;
+            const float iou = iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
+            if (!(iou <= iou_thres)) lremoved[j] = 1;
+          }
+        }
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) s_kept = kept;
+      break;
+    }
+
+    // Candidates [jlo, jhi) (sorted positions, not yet removed) against kept boxes [klo, khi): all 1024
+    // threads, thread = (candidate, split of the kept list).  Each wave holds 64 consecutive candidates
+    // and one split, so every lane of a wave reads the same kept boxes (LDS broadcast), 4 per batch of
+    // loads; a suppressed candidate's flag is set by whichever split finds it (all writers store 1).
+    auto test_range = [&](int jlo, int jhi, int klo, int khi) {
+      const int nj = jhi - jlo, nk = khi - klo;
+      if (nj <= 0 || nk <= 0 || stop == 5) return;  // 5: diagnostics only (skips the tests)
+      const int rj = (nj + 63) & ~63;
+      const int S = max(1, min(nk, NMS_THREADS / rj));
+      for (int idx = threadIdx.x; idx < rj * S; idx += NMS_THREADS) {
+        const int j = jlo + idx % rj, sp0 = idx / rj;
+        if (j >= jhi || lremoved[j]) continue;
+        const int c = sp(j);
+        const float4 bj = w.cbox[c];
+        const float aj = w.carea[c];
+        bool rem = false;
+        int k = klo + sp0;
+        for (; k + 3 * S < khi && !rem; k += 4 * S) {
+          float4 kb[4];
+          float ka[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            kb[u] = kbox[k + u * S];
+            ka[u] = karea[k + u * S];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rem |= suppresses(kb[u], ka[u], bj, aj, iou_thres);
+        }
+        for (; k < khi && !rem; k += S) rem = suppresses(kbox[k], karea[k], bj, aj, iou_thres);
+        if (rem) lremoved[j] = 1;
+      }
+    };
+
     // ---- 3a. tiled greedy with a lazy frontier (exact when every area > 0)
+    uint64_t* colmask = tile_sup;  // colmask[u] = {t < u in the tile : IoU(t, u) > thr}
     int cursor = 0, F = 0;
-    uint64_t tm[6] = {0, 0, 0, 0, 0, 0}, tprev = stop == 9 ? __builtin_amdgcn_s_memtime() : 0;
-    auto tick = [&](int slot) {  // diagnostics (FCE_NMS_STOP=9): barrier-to-barrier segment clocks
+    // diagnostics (FCE_NMS_STOP=9): s_memtime clocks per segment [select, colmask, resolve, window
+    // test, tiles, extensions, extension tests, emit] written to dets[n][0..1][..] (8 floats)
+    uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = stop == 9 ? __builtin_amdgcn_s_memtime() : 0;
+    auto tick = [&](int slot) {
       if (stop == 9) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tm[slot] += t - tprev;
         tprev = t;
       }
     };
+    bool reached = false;  // max_det reached
     while (true) {
       // select the next <= 64 surviving candidates in [cursor, F), extending F while short
       while (true) {
@@ -408,15 +502,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
           for (int c = cursor; cnt < TILE && c < F; c += 64) {
             const int j = c + lane;
             const bool alive = j < F && !lremoved[j];
-            const uint64_t b = __ballot(alive);
-            const int take = min(__popcll(b), TILE - cnt);
-            const int rank = __popcll(b & ((1ull << lane) - 1ull));
+            const uint64_t bb = __ballot(alive);
+            const int take = min(__popcll(bb), TILE - cnt);
+            const int rank = __popcll(bb & ((1ull << lane) - 1ull));
             if (alive && rank < take) tile_idx[cnt + rank] = j;
             cnt += take;
           }
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile_idx writes have landed
           __builtin_amdgcn_wave_barrier();
-          const bool need = cnt < TILE && F < M;
+          const bool need = cnt < TILE && F < Mg;
           if (!need && lane < cnt) {
             const int c = sp(tile_idx[lane]);
             tile_box[lane] = w.cbox[c];
@@ -425,63 +519,63 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
           if (lane == 0) {
             s_tile_n = cnt;
             s_need = need;
-            s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : M;
+            s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : Mg;
           }
         }
         __syncthreads();
         tick(0);
         if (!s_need) break;
-        // candidates entering the window: test once against every box kept so far
-        const int Fn = min(M, F + WIN), nkept = s_kept;
-        for (int jb = F + wv * 64; jb < Fn; jb += NMS_THREADS) {  // wave-uniform trip count
-          const int j = jb + lane;
-          const bool act = j < Fn;
-          float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
-          float aj = 0.f;
-          if (act) {
-            const int c = sp(j);
-            bj = w.cbox[c];
-            aj = w.carea[c];
-          }
-          const bool rem = kept_suppress(bj, aj, act, 0, nkept);
-          if (act) lremoved[j] = rem;
-        }
+        // candidates entering the window: tested once against every box kept so far
+        const int Fn = min(Mg, F + WIN);
+        for (int j = F + threadIdx.x; j < Fn; j += NMS_THREADS) lremoved[j] = 0;
+        __syncthreads();
+        test_range(F, Fn, 0, s_kept);
         F = Fn;
         __syncthreads();
-        tick(1);
+        tm[5] += 1;
+        tick(6);
       }
+      tm[4] += 1;
       const int cnt = s_tile_n;
       if (cnt == 0) break;
-      // suppression rows of the tile: sup[t] = {u > t : IoU(t, u) > thr}
-      for (int t = wv; t < cnt; t += NWAVES) {
+      // column masks of the tile's suppression relation: wave w owns columns u = w, w+16, ..; lane = row t
+      for (int u = wv; u < TILE && stop != 6; u += NWAVES) {  // 6: diagnostics only
         bool sup = false;
-        if (lane > t && lane < cnt) sup = suppresses(tile_box[t], tile_area[t], tile_box[lane], tile_area[lane], iou_thres);
-        const uint64_t b = __ballot(sup);
-        if (lane == 0) tile_sup[t] = b;
+        if (lane < u && u < cnt)
+          sup = suppresses(tile_box[lane], tile_area[lane], tile_box[u], tile_area[u], iou_thres);
+        const uint64_t bb = __ballot(sup);
+        if (lane == 0) colmask[u] = bb;
       }
       __syncthreads();
-      tick(2);
+      tick(1);
       if (wv == 0) {
+        // greedy over the tile as a fixpoint (lane u = tile candidate u): u is kept once none of its
+        // suppressors is kept or undecided, removed once one of them is kept.  Every round decides at
+        // least the lowest undecided candidate, and each decision is the sequential greedy's.
         const int kept0 = s_kept;
-        const uint64_t mysup = lane < cnt ? tile_sup[lane] : 0ull;
-        const uint32_t sup_lo = uint32_t(mysup), sup_hi = uint32_t(mysup >> 32);
-        uint64_t removed = 0, keptm = 0;
-        int nk = 0;
-        bool done = false;
-        for (int t = 0; t < cnt; ++t) {  // wave-uniform: SALU bit ops + v_readlane
-          if ((removed >> t) & 1ull) continue;
-          keptm |= 1ull << t;
-          ++nk;
-          if (kept0 + nk >= max_det) {
-            done = true;
-            break;
-          }
-          // readlane returns int: go through uint32_t so bit 31 does not sign-extend
-          removed |= uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sup_lo), t))) |
-                     (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sup_hi), t))) << 32);
+        const uint64_t C = lane < cnt ? colmask[lane] : 0ull;
+        uint64_t undecided = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull), kept = 0;
+        while (undecided) {
+          const bool me = (undecided >> lane) & 1ull;
+          const uint64_t k = __ballot(me && (C & (kept | undecided)) == 0ull);
+          const uint64_t r = __ballot(me && (C & kept) != 0ull);
+          kept |= k;
+          undecided &= ~(k | r);
         }
-        if ((keptm >> lane) & 1ull) {
-          const int r = __popcll(keptm & ((1ull << lane) - 1ull));
+        // max_det: the greedy stops at the (max_det - kept0)-th kept candidate of the tile
+        int nk = __popcll(kept);
+        bool done = false;
+        if (kept0 + nk >= max_det) {
+          const int allow = max_det - kept0;
+          uint64_t m = kept;
+          for (int i = 0; i < allow - 1; ++i) m &= m - 1ull;  // drop the lowest allow-1 bits
+          const uint64_t last = m & (~m + 1ull);               // the allow-th kept candidate
+          kept &= (last << 1) - 1ull;
+          nk = allow;
+          done = true;
+        }
+        if ((kept >> lane) & 1ull) {
+          const int r = __popcll(kept & ((1ull << lane) - 1ull));
           kbox[kept0 + r] = tile_box[lane];
           karea[kept0 + r] = tile_area[lane];
           kidx[kept0 + r] = sp(tile_idx[lane]);
@@ -489,69 +583,30 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
         if (lane == 0) {
           s_nk = nk;
           s_kept = kept0 + nk;
-          s_done = done || s_next >= M;
+          s_done = done ? 2 : (s_next >= Mg ? 1 : 0);
         }
       }
       __syncthreads();
-      tick(3);
-      if (s_done) break;
-      // the rest of the window against the tile's kept boxes
-      const int k0 = s_kept - s_nk, k1 = s_kept, start = s_next;
-      for (int jb = start + wv * 64; jb < F; jb += NMS_THREADS) {  // wave-uniform trip count
-        const int j = jb + lane;
-        const bool act = j < F && !lremoved[j];
-        float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
-        float aj = 0.f;
-        if (act) {
-          const int c = sp(j);
-          bj = w.cbox[c];
-          aj = w.carea[c];
-        }
-        if (kept_suppress(bj, aj, act, k0, k1)) lremoved[j] = 1;
+      tick(2);
+      if (s_done) {
+        reached = s_done == 2;
+        break;
       }
+      // the rest of the window against the tile's kept boxes
+      const int start = s_next;
+      test_range(start, F, s_kept - s_nk, s_kept);
       cursor = start;
       __syncthreads();
-      tick(4);
-      tm[5] += 1;
+      tick(3);
     }
     __syncthreads();
+    tick(7);
     for (int slot = threadIdx.x; slot < s_kept; slot += NMS_THREADS) emit_det(kidx[slot], slot);
-    if (stop == 9 && threadIdx.x == 0)
-      for (int i = 0; i < 6; ++i) dets[int64_t(n) * max_det * 6 + i] = float(tm[i]);
-  } else {
-    // ---- 3b. literal per-box greedy (TorchNMS.nms with its early exit) for degenerate boxes
-    for (int i = threadIdx.x; i < M; i += NMS_THREADS) lremoved[i] = 0;
     __syncthreads();
-    int kept = 0;
-    for (int i = 0; i < M && kept < max_det; ++i) {
-      if (lremoved[i]) continue;
-      const int ci = sp(i);
-      if (threadIdx.x == 0) emit_det(ci, kept);
-      ++kept;
-      if (kept >= max_det) break;
-      const float4 bi = w.cbox[ci];
-      const float ai = w.carea[ci];
-      int any = 0;
-      for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
-        if (lremoved[j]) continue;
-        const int cj = sp(j);
-        float inter;
-        iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
-        any |= inter != 0.0f;
-      }
-      any = __syncthreads_or(any);
-      if (any) {
-        for (int j = i + 1 + threadIdx.x; j < M; j += NMS_THREADS) {
-          if (lremoved[j]) continue;
-          const int cj = sp(j);
-          float inter;
-          const float iou = iou_ref(bi, ai, w.cbox[cj], w.carea[cj], &inter);
-          if (!(iou <= iou_thres)) lremoved[j] = 1;
-        }
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) s_kept = kept;
+    tick(7);
+    if (stop == 9 && threadIdx.x == 0)
+      for (int i = 0; i < 8; ++i) dets[int64_t(n) * max_det * 6 + i] = float(tm[i]);
+    break;
   }
   __syncthreads();
   if (threadIdx.x == 0) counts[n] = s_kept;
@@ -559,7 +614,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
 
 int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
         void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s) {
-  FCE_CHECK(nc >= 1 && A >= 0 && max_det >= 1 && max_nms >= 1, "nms: bad sizes");
+  FCE_CHECK(nc >= 1 && nc <= 65535 && A >= 0 && max_det >= 1 && max_nms >= 1, "nms: bad sizes");
   FCE_CHECK(max_nms <= REMOVED_CAP, "nms: max_nms > 32768 unsupported");
   FCE_CHECK(conf >= 0.f && conf <= 1.f && iou >= 0.f && iou <= 1.f, "nms: thresholds must be in [0, 1]");
   if (n == 0) return FCE_OK;

@@ -131,3 +131,52 @@ def non_max_suppression(pred: torch.Tensor, conf_thres=0.25, iou_thres=0.7, max_
     nms(pred)
     dets, keep = nms.results()
     return (dets, keep) if return_idxs else dets
+
+
+class Pipeline:
+    """Batch pipeline: forward of batch i+1 overlaps the NMS of batch i.
+
+    The forward runs on the caller's stream into one of `depth` pred buffers; the NMS of that buffer runs
+    on a side stream after an event.  A buffer (and its NMS outputs) is reused only after the NMS that
+    read it has finished (event wait on the caller's stream), so every batch gets exactly the forward +
+    NMS of the sequential path — the NMS latency (one workgroup per image) just hides under the next
+    forward.  `submit(x)` returns the slot whose `NMS` object holds that batch's results once
+    `wait(slot)` (or a device sync) has passed.
+    """
+
+    def __init__(self, engine: Engine, depth: int = 2, **nms_kw):
+        self.eng, self.depth = engine, depth
+        dev = engine.device
+        self.preds = [torch.empty_like(engine.pred) for _ in range(depth)]
+        self.nms = [NMS(engine.batch, engine.anchors, engine.nc, dev, **nms_kw) for _ in range(depth)]
+        self.side = torch.cuda.Stream(dev)
+        self.fwd_done = [torch.cuda.Event() for _ in range(depth)]
+        self.nms_done = [torch.cuda.Event() for _ in range(depth)]
+        self.used = [False] * depth
+        self.i = 0
+
+    def submit(self, x: torch.Tensor) -> int:
+        k = self.i % self.depth
+        self.i += 1
+        main = torch.cuda.current_stream(self.eng.device)
+        if self.used[k]:
+            main.wait_event(self.nms_done[k])  # pred[k] / nms[k] free again
+        self.eng(x, out=self.preds[k])
+        self.fwd_done[k].record(main)
+        self.side.wait_event(self.fwd_done[k])
+        with torch.cuda.stream(self.side):
+            self.nms[k](self.preds[k])
+            self.nms_done[k].record(self.side)
+        self.used[k] = True
+        return k
+
+    def wait(self, k: int | None = None):
+        """Make the caller's stream wait for the NMS of slot k (all slots when None)."""
+        main = torch.cuda.current_stream(self.eng.device)
+        for j in range(self.depth) if k is None else (k,):
+            if self.used[j]:
+                main.wait_event(self.nms_done[j])
+
+    def results(self, k: int):
+        self.nms_done[k].synchronize()
+        return self.nms[k].results()

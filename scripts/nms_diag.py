@@ -24,7 +24,7 @@ pred = eng(x).clone()
 nms = NMS(B, eng.anchors, eng.nc, dev)
 ncand = (pred[:, 4:].amax(1) > 0.25).sum(1)
 print("candidates per image: min", int(ncand.min()), "max", int(ncand.max()), "of", eng.anchors, flush=True)
-for stop in ("1", "2", "3", "0"):
+for stop in ("1", "2", "5", "3", "0"):
     os.environ["FCE_NMS_STOP"] = stop
     for _ in range(3):
         nms(pred)
@@ -40,7 +40,7 @@ print("kept", nms.counts.tolist()[:8])
 os.environ["FCE_NMS_STOP"] = "9"
 nms(pred)
 torch.cuda.synchronize()
-t = nms.dets[:4, 0, :].cpu().tolist()
-print("segment clocks [select, extend, sup, resolve, window, tiles] (s_memtime):")
+t = nms.dets[:4, :2, :].reshape(4, 12)[:, :8].cpu().tolist()
+print("segment clocks [select, colmask, resolve, window, tiles, extensions, ext-tests, tail] (s_memtime):")
 for r in t:
     print("  ", [int(v) for v in r])

@@ -17,7 +17,7 @@ import torch
 import cases
 from fce_yolo_amd import _native as N
 from fce_yolo_amd import modules as M
-from fce_yolo_amd.engine import Engine, non_max_suppression
+from fce_yolo_amd.engine import NMS, Engine, Pipeline, non_max_suppression
 from oracle import nms_oracle
 
 pytestmark = pytest.mark.gpu
@@ -204,3 +204,53 @@ def test_nms_large_candidate_set_global_sort(device):
         od, ok = nms_oracle.non_max_suppression(p, max_nms=max_nms)
         assert np.array_equal(keep[0].cpu().numpy(), ok[0]) and np.array_equal(dets[0].cpu().numpy(), od[0])
 
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_nms_clustered_suppression_chains(seed, device):
+    """Heavy, chained suppression: jittered boxes around a few centres, few classes, tied (quantised)
+    scores; several IoU thresholds and max_det values.  Kept indices and rows bit-exact vs the oracle."""
+    rng = np.random.default_rng(100 + seed)
+    B, A, nc = 4, (4000, 1500, 900)[seed], 3  # full sort / 2048-slot / 1024-slot small-set sort
+    p = np.zeros((B, 4 + nc, A), np.float32)
+    for b in range(B):
+        centres = rng.random((12, 2)) * 600 + 20
+        k = rng.integers(0, 12, A)
+        p[b, 0:2] = (centres[k] + rng.normal(0, 6, (A, 2))).T
+        p[b, 2:4] = (rng.random((A, 2)) * 30 + 40).T
+        cls = rng.integers(0, nc, A)
+        p[b, 4 + cls, np.arange(A)] = np.round(rng.random(A) * 64) / 64  # ties on purpose
+    pt = torch.from_numpy(p).to(device)
+    for iou, max_det in ((0.7, 300), (0.5, 300), (0.3, 50), (0.9, 1000), (0.7, 7)):
+        dets, keep = non_max_suppression(pt, 0.25, iou, max_det, return_idxs=True)
+        od, ok = nms_oracle.non_max_suppression(p, 0.25, iou, max_det=max_det)
+        for b in range(B):
+            assert np.array_equal(keep[b].cpu().numpy(), ok[b]), (iou, max_det, b)
+            assert np.array_equal(dets[b].cpu().numpy(), od[b]), (iou, max_det, b)
+
+
+def test_pipeline_overlap_matches_sequential(device):
+    """engine.Pipeline (forward i+1 overlapping NMS i, double-buffered) gives every batch exactly the
+    sequential forward + NMS result."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    B, S = 4, 320
+    eng = Engine(model, B, S, device)
+    xs = [torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(500 + i)).half().to(device) for i in range(5)]
+    seq = []
+    nms = NMS(B, eng.anchors, eng.nc, device)
+    for x in xs:
+        nms(eng(x))
+        d, k = nms.results()
+        seq.append(([t.clone() for t in d], [t.clone() for t in k]))
+    pipe = Pipeline(eng, depth=2)
+    got = [pipe.submit(x) for x in xs]  # back to back; only the last `depth` batches remain in their slots
+    for i in range(len(xs) - 2, len(xs)):
+        d, k = pipe.results(got[i])
+        for b in range(B):
+            assert torch.equal(d[b], seq[i][0][b]) and torch.equal(k[b], seq[i][1][b]), (i, b)
+    # and every batch, by draining after each submit
+    pipe2 = Pipeline(eng, depth=2)
+    for i, x in enumerate(xs):
+        d, k = pipe2.results(pipe2.submit(x))
+        for b in range(B):
+            assert torch.equal(d[b], seq[i][0][b]) and torch.equal(k[b], seq[i][1][b]), (i, b)
