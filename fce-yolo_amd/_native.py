@@ -93,6 +93,8 @@ _SIGS = {
     "fce_conv_weight_bytes": (_SZ, [_PCD]),
     "fce_conv_pack_weights": (_I, [_PCD, _P, _P]),
     "fce_conv2d": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _P]),
+    "fce_conv_variants": (_I, [_PCD, _I, _P, _I]),
+    "fce_conv2d_variant": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _I, _P]),
     "fce_conv2d_detect": (_I, [_PCD, _PT, _P, _P, C.POINTER(DetectEpi), _P]),
     "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),
     "fce_weighted_add": (_I, [_PT, _I, _P, _I, _I, _I, _PT, _P]),
@@ -121,6 +123,8 @@ _SIGS = {
     "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),
     "fce_net_profile": (_I, [_P, _PT, _P, _P, _P, _I, _P]),
     "fce_net_num_ops": (_I, [_P]),
+    "fce_net_op_variant": (_I, [_P, _I]),
+    "fce_net_tune_record": (_I, [_P, _I, _P, _P, _P]),
     "fce_net_op_info": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fce_net_buffer": (_I, [_P, _I, _PT]),
 }

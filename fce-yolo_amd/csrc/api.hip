@@ -91,6 +91,15 @@ int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w, const
   FCE_CHECK(d && x && w && bias && y, "fce_conv2d: null argument");
   FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream));)
 }
+int fce_conv_variants(const fce_conv_desc* d, int in_w, int* codes, int cap) {
+  if (!d || !codes || cap <= 0) return 0;
+  return conv_tile_candidates(*d, 0, in_w, codes, cap);
+}
+int fce_conv2d_variant(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
+                       const fce_tensor* res, const fce_tensor* y, int variant, void* stream) {
+  FCE_CHECK(d && x && w && bias && y, "fce_conv2d_variant: null argument");
+  FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream), variant);)
+}
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
                       const fce_detect_epi* e, void* stream) {
   FCE_CHECK(d && x && w && bias && e, "fce_conv2d_detect: null argument");
@@ -186,6 +195,11 @@ struct OpDesc {
 struct fce_net {
   std::vector<BufDesc> bufs;
   std::vector<OpDesc> ops;
+  struct TuneRec {
+    int op, code;
+    float ms;
+  };
+  std::vector<TuneRec> tune_log;  // plan-time autotune measurements (fce_net_tune_record)
   int batch = 0, H = 0, W = 0;
   char* arena = nullptr;
   size_t arena_bytes = 0;
@@ -703,6 +717,7 @@ static int autotune(fce_net* net) {
       if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
+      if (st == FCE_OK) net->tune_log.push_back({int(&op - net->ops.data()), cand[i], ms / 3.f});
       if (st == FCE_OK && ms < best_ms) {
         best_ms = ms;
         best = cand[i];
@@ -721,6 +736,7 @@ int fce_net_plan(fce_net* net, int batch, int h, int w) {
   FCE_CHECK(h % 32 == 0 && w % 32 == 0, "fce_net_plan: H and W must be multiples of 32 (max stride)");
   FCE_GUARD({
     net->release();
+    net->tune_log.clear();
     net->batch = batch;
     net->H = h;
     net->W = w;
@@ -893,6 +909,18 @@ int fce_net_op_info(const fce_net* net, int i, char* name, int cap, double* byte
     name[n] = 0;
   }
   return FCE_OK;
+}
+
+int fce_net_op_variant(const fce_net* net, int i) {
+  return net && i >= 0 && i < int(net->ops.size()) ? net->ops[i].tile : -1;
+}
+
+int fce_net_tune_record(const fce_net* net, int k, int* op, int* code, float* ms) {
+  if (!net || k < 0 || k >= int(net->tune_log.size())) return 0;
+  if (op) *op = net->tune_log[k].op;
+  if (code) *code = net->tune_log[k].code;
+  if (ms) *ms = net->tune_log[k].ms;
+  return 1;
 }
 
 int fce_net_buffer(const fce_net* net, int id, fce_tensor* out) {

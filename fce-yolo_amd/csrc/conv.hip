@@ -136,6 +136,138 @@ struct ConvDepth {
   static constexpr int D = RC * RP == 1 ? 8 : RC * RP == 2 ? 4 : 2;
 };
 
+// Epilogue of the dense MFMA kernels: acc[r][p] = 16 couts (cout tile cot0 + r) x 16 pixels
+// (pix_base + 16 p ..) of this wave; lane = (col = pixel, grp = 4-cout group).  Bias, SiLU, residual,
+// BiFPN weighted store / accumulate, or the fused Detect DFL / cls-sigmoid tails.
+template <int RC, int RP, int OUT>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][RP], int pix_base, int cot0, int col,
+                                              int grp) {
+  const int cotiles = (a.cout + 15) >> 4;
+  if (OUT == OUT_DFL) {
+    // Detect box branch (head.py:161-162, block.py:76-79, tal.py:367-376): the 4 x 16 logits of a
+    // pixel live in tiles r = side, lanes {p, p+16, p+32, p+48} x 4 registers -> softmax expectation
+    // with two xor-shuffles, then xywh * stride into pred rows 0..3 (fp32 throughout).
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      float dist[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v[4], mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[r < RC ? r : 0][p][j] + a.bias[r * 16 + grp * 4 + j];
+          mx = fmaxf(mx, v[j]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float den = 0.f, num = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = expf(v[j] - mx);
+          den += e;
+          num = __fadd_rn(num, __fmul_rn(e, (float)(grp * 4 + j)));  // no FMA: match detect_decode
+        }
+        den += __shfl_xor(den, 16);
+        den += __shfl_xor(den, 32);
+        num += __shfl_xor(num, 16);
+        num += __shfl_xor(num, 32);
+        dist[r] = num / den;
+      }
+      const int pix = pix_base + p * 16 + col;
+      if (grp == 0 && pix < a.P) {
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        const float ax = (float)(q % a.det_w) + 0.5f, ay = (float)(q / a.det_w) + 0.5f;
+        const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
+        float* o = a.pred + int64_t(n) * (4 + a.det_nc) * a.det_A + a.det_a0 + q;
+        o[0] = (x1 + x2) / 2.0f * a.det_stride;
+        o[a.det_A] = (y1 + y2) / 2.0f * a.det_stride;
+        o[int64_t(2) * a.det_A] = (x2 - x1) * a.det_stride;
+        o[int64_t(3) * a.det_A] = (y2 - y1) * a.det_stride;
+      }
+    }
+    return;
+  }
+  if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int co0 = (cot0 + r) * 16 + grp * 4;
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        const int pix = pix_base + p * 16 + col;
+        if (pix >= a.P) continue;
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) o[int64_t(co0 + j) * a.det_A] = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+      }
+    }
+    return;
+  }
+  float alpha = 1.f;
+  if (OUT == OUT_WSTORE || OUT == OUT_ACCUM) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co0 = (cot0 + r) * 16 + grp * 4;
+    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int pix = pix_base + p * 16 + col;
+      if (pix >= a.P) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(t) : t;
+      }
+      if (OUT == OUT_F32) {
+        float* yo = static_cast<float*>(a.y) + int64_t(pix) * a.ycs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          *reinterpret_cast<f4*>(yo) = f4{v[0], v[1], v[2], v[3]};
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) yo[j] = v[j];
+        }
+        continue;
+      }
+      _Float16* yo = static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co0;
+      if (a.res) {
+        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] += (float)ro[j];
+        }
+      }
+      if (OUT == OUT_WSTORE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= alpha;
+      }
+      if (a.vec_ok && co0 + 3 < a.cout) {
+        if (OUT == OUT_ACCUM) {
+          h4 pv4 = *reinterpret_cast<const h4*>(yo);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (float)pv4[j] + alpha * v[j];
+        }
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      } else {
+        for (int j = 0; j < 4; ++j) {
+          if (co0 + j >= a.cout) continue;
+          float t = v[j];
+          if (OUT == OUT_ACCUM) t = (float)yo[j] + alpha * t;
+          yo[j] = (_Float16)t;
+        }
+      }
+    }
+  }
+}
+
 template <int KS, int RC, int RP, int OUT, bool FAST>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   constexpr int D = ConvDepth<RC, RP>::D;
@@ -273,129 +405,124 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  if (OUT == OUT_DFL) {
-    // Detect box branch (head.py:161-162, block.py:76-79, tal.py:367-376): the 4 x 16 logits of a
-    // pixel live in tiles r = side, lanes {p, p+16, p+32, p+48} x 4 registers -> softmax expectation
-    // with two xor-shuffles, then xywh * stride into pred rows 0..3 (fp32 throughout).
-#pragma unroll
-    for (int p = 0; p < RP; ++p) {
-      float dist[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v[4], mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = acc[r < RC ? r : 0][p][j] + a.bias[r * 16 + grp * 4 + j];
-          mx = fmaxf(mx, v[j]);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        float den = 0.f, num = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float e = expf(v[j] - mx);
-          den += e;
-          num = __fadd_rn(num, __fmul_rn(e, (float)(grp * 4 + j)));  // no FMA: match detect_decode
-        }
-        den += __shfl_xor(den, 16);
-        den += __shfl_xor(den, 32);
-        num += __shfl_xor(num, 16);
-        num += __shfl_xor(num, 32);
-        dist[r] = num / den;
-      }
-      const int pix = pix_base + p * 16 + col;
-      if (grp == 0 && pix < a.P) {
-        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
-        const float ax = (float)(q % a.det_w) + 0.5f, ay = (float)(q / a.det_w) + 0.5f;
-        const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
-        float* o = a.pred + int64_t(n) * (4 + a.det_nc) * a.det_A + a.det_a0 + q;
-        o[0] = (x1 + x2) / 2.0f * a.det_stride;
-        o[a.det_A] = (y1 + y2) / 2.0f * a.det_stride;
-        o[int64_t(2) * a.det_A] = (x2 - x1) * a.det_stride;
-        o[int64_t(3) * a.det_A] = (y2 - y1) * a.det_stride;
-      }
-    }
-    return;
-  }
-  if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
-#pragma unroll
-    for (int r = 0; r < RC; ++r) {
-      const int co0 = (cot0 + r) * 16 + grp * 4;
-#pragma unroll
-      for (int p = 0; p < RP; ++p) {
-        const int pix = pix_base + p * 16 + col;
-        if (pix >= a.P) continue;
-        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
-        float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) o[int64_t(co0 + j) * a.det_A] = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
-      }
-    }
-    return;
-  }
-  float alpha = 1.f;
-  if (OUT == OUT_WSTORE || OUT == OUT_ACCUM) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+  conv_epilogue<RC, RP, OUT>(a, acc, pix_base, cot0, col, grp);
+}
+
+// ============================================================================ 1x1, streaming waves
+// For 1x1 convs with cin % 32 == 0 and few K-steps (cin <= 32 * NSM): in the implicit-GEMM kernel a
+// wave then does a handful of MFMAs behind one load latency and exits.  Here a wave keeps the weight
+// fragments of its RC cout tiles for ALL K-steps in registers (loaded once) and walks a strided
+// sequence of pixel tiles (RP x 16 pixels), the next tile's B fragments in flight while the current
+// tile's MFMAs and epilogue run.  Waves gw of a launch: cout group gw % gy, tile sequence
+// gw / gy, + W, + 2W, ...  (adjacent waves = the cout groups of the same pixels, on one CU).  Per
+// output the K order is the implicit-GEMM kernel's (steps 0..nsteps-1): bitwise-identical results.
+template <int RC, int RP, int NSM, int OUT>
+__global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvArgs a, int W) {
+  const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int g = gw % a.gy, i0 = gw / a.gy;
+  const int ns = a.nsteps;
+  const int cot0 = g * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  const int ntiles = (a.P + 16 * RP - 1) / (16 * RP);
+  h8 aw[NSM][RC];
 #pragma unroll
   for (int r = 0; r < RC; ++r) {
-    const int co0 = (cot0 + r) * 16 + grp * 4;
-    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
-    float bz[4];
+    const h8* wf = reinterpret_cast<const h8*>(a.w) + (size_t(min(cot0 + r, cotiles - 1)) * a.nalloc) * 64 + lane;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+    for (int st = 0; st < NSM; ++st) aw[st][r] = st < ns ? wf[st * 64] : h8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const int hw = a.Ho * a.Wo;
+  auto load_tile = [&](int t, h8 (&b)[NSM][RP]) {
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
-      const int pix = pix_base + p * 16 + col;
-      if (pix >= a.P) continue;
-      float v[4];
+      int pix = t * 16 * RP + p * 16 + col;
+      pix = pix < a.P ? pix : 0;  // past the end: any valid pixel (the epilogue skips it)
+      const int n = pix / hw, r = pix - n * hw;
+      const int oy = r / a.Wo, ox = r - oy * a.Wo;
+      const _Float16* src = a.x + nhwc_off(n, oy >> a.up, ox >> a.up, a.Hs, a.Ws, a.xcs) + grp * 8;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float t = acc[r][p][j] + bz[j];
-        v[j] = a.act ? silu(t) : t;
-      }
-      if (OUT == OUT_F32) {
-        float* yo = static_cast<float*>(a.y) + int64_t(pix) * a.ycs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          *reinterpret_cast<f4*>(yo) = f4{v[0], v[1], v[2], v[3]};
-        } else {
-          for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) yo[j] = v[j];
-        }
-        continue;
-      }
-      _Float16* yo = static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co0;
-      if (a.res) {
-        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          h4 rv = *reinterpret_cast<const h4*>(ro);
+      for (int st = 0; st < NSM; ++st)
+        if (st < ns) b[st][p] = *reinterpret_cast<const h8*>(src + st * 32);
+    }
+  };
+  h8 bq[NSM][RP];
+  if (i0 < ntiles) load_tile(i0, bq);
+  for (int t = i0; t < ntiles; t += W) {
+    h8 bc[NSM][RP];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
-        } else {
-          for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] += (float)ro[j];
-        }
-      }
-      if (OUT == OUT_WSTORE) {
+    for (int st = 0; st < NSM; ++st)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] *= alpha;
-      }
-      if (a.vec_ok && co0 + 3 < a.cout) {
-        if (OUT == OUT_ACCUM) {
-          h4 pv4 = *reinterpret_cast<const h4*>(yo);
+      for (int p = 0; p < RP; ++p) bc[st][p] = bq[st][p];
+    if (t + W < ntiles) load_tile(t + W, bq);
+    f4 acc[RC][RP];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (float)pv4[j] + alpha * v[j];
-        }
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-      } else {
-        for (int j = 0; j < 4; ++j) {
-          if (co0 + j >= a.cout) continue;
-          float t = v[j];
-          if (OUT == OUT_ACCUM) t = (float)yo[j] + alpha * t;
-          yo[j] = (_Float16)t;
-        }
+    for (int r = 0; r < RC; ++r)
+#pragma unroll
+      for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NSM; ++st) {
+      if (st < ns) {
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aw[st][r], bc[st][p], acc[r][p], 0, 0, 0);
       }
     }
+    conv_epilogue<RC, RP, OUT>(a, acc, t * 16 * RP, cot0, col, grp);
   }
+}
+
+static bool stream_ok(int nsm, int rc, int rp) { return nsm * (rc + 2 * rp) <= 40; }
+
+template <int RC, int RP, int NSM>
+static void launch_stream_o(const ConvArgs& a, int out_kind, dim3 grid, int W, hipStream_t s) {
+#define STREAM_L(O) FCE_LAUNCH((conv1x1_stream_kernel<RC, RP, NSM, O>), grid, dim3(256), 0, s, a, W)
+  switch (out_kind) {
+    case OUT_F16: STREAM_L(OUT_F16); break;
+    case OUT_F32: STREAM_L(OUT_F32); break;
+    case OUT_WSTORE: STREAM_L(OUT_WSTORE); break;
+    case OUT_DFL: STREAM_L(OUT_DFL); break;
+    case OUT_CLS: STREAM_L(OUT_CLS); break;
+    default: STREAM_L(OUT_ACCUM); break;
+  }
+#undef STREAM_L
+}
+
+template <int NSM>
+static void launch_stream_n(const ConvArgs& a, int out_kind, int rc, int rp, dim3 grid, int W, hipStream_t s) {
+  if constexpr (NSM <= 4) {
+    if (rc == 4 && rp == 2) return launch_stream_o<4, 2, NSM>(a, out_kind, grid, W, s);
+    if (rc == 2 && rp == 2) return launch_stream_o<2, 2, NSM>(a, out_kind, grid, W, s);
+    if (rc == 4 && rp == 1) return launch_stream_o<4, 1, NSM>(a, out_kind, grid, W, s);
+  }
+  if (rc == 1 && rp == 2) return launch_stream_o<1, 2, NSM>(a, out_kind, grid, W, s);
+  if (rc == 2 && rp == 1) return launch_stream_o<2, 1, NSM>(a, out_kind, grid, W, s);
+  launch_stream_o<1, 1, NSM>(a, out_kind, grid, W, s);
+}
+
+static int stream_nsm(int nsteps) { return nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 8 ? 8 : 0; }
+
+// waves per cout group: enough pixel-tile streams to fill the GPU (about 8 waves per SIMD in all),
+// but every wave gets at least 2 tiles so the prefetch has something to overlap
+static int launch_stream(const ConvArgs& a0, int out_kind, int rc, int rp, hipStream_t s) {
+  const int nsm = stream_nsm(a0.nsteps);
+  FCE_CHECK(nsm > 0 && stream_ok(nsm, rc, rp), "conv 1x1 stream: K too deep for the register budget");
+  ConvArgs a = a0;
+  const int cotiles = (a.cout + 15) / 16;
+  a.gy = (cotiles + rc - 1) / rc;
+  const int ntiles = (a.P + 16 * rp - 1) / (16 * rp);
+  int W = std::max(1, std::min((ntiles + 1) / 2, 8192 / a.gy));
+  while ((int64_t(W) * a.gy) % 4) ++W;  // whole blocks of 4 waves
+  const dim3 grid(unsigned(int64_t(W) * a.gy / 4));
+  if (nsm == 2)
+    launch_stream_n<2>(a, out_kind, rc, rp, grid, W, s);
+  else if (nsm == 4)
+    launch_stream_n<4>(a, out_kind, rc, rp, grid, W, s);
+  else
+    launch_stream_n<8>(a, out_kind, rc, rp, grid, W, s);
+  return launch_status("conv1x1_stream_kernel");
 }
 
 // ============================================================================ 3x3, LDS halo tiles
@@ -507,6 +634,132 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+// ============================================================================ 3x3, small cin, LDS tiles
+// For cin % 8 == 0 and cin % 32 != 0 (cin <= 64: the C3k2 bottlenecks and early convs of small models,
+// e.g. 8 -> 8 at 160 x 160).  Same block / wave geometry as conv3x3_tile_kernel, but the whole input
+// tile + halo with ALL cin channels ((TH-1)*S+3 x (TW-1)*S+3 pixels x cin*2 B) is staged in LDS once,
+// and the K loop walks the implicit-GEMM kernel's tap-major 8-channel chunks (c = 4 s + lane/16,
+// tap = c / cpt): the same A fragments and the same per-output summation order as conv_mfma_kernel, so
+// the two give bitwise-identical results.  Input pixels are read from HBM once (plus halo) instead of
+// once per tap from L2.
+template <int S, int RC, int RP>
+__global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
+  constexpr int TW = 16, TH = 4 * RP;
+  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
+  extern __shared__ __attribute__((aligned(16))) h8 stile[];  // [RI][CI][cpt]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int cpt = a.cpt;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int n = t / tiles_y;
+  const int ox0 = tx * TW, oy0 = ty * TH;
+  const int cot0 = blockIdx.y * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  const h8* wfrag[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int ct = min(cot0 + r, cotiles - 1);
+    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
+  }
+  // A fragments of step 0 in flight while the tile is staged
+  h8 an[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) an[r] = wfrag[r][0];
+  const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const int ne = RI * CI * cpt;
+  for (int e = threadIdx.x; e < ne; e += 256) {
+    const int pc = e / cpt, q = e - pc * cpt;
+    const int r = pc / CI, c = pc - r * CI;
+    const int iy = iy0 + r, ix = ix0 + c;
+    h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws)
+      v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + q * 8);
+    stile[e] = v;
+  }
+  __syncthreads();
+  f4 acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  const h8 zero = h8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int st = 0; st < a.nsteps; ++st) {
+    h8 af[RC];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) af[r] = an[r];
+    if (st + 1 < a.nsteps) {
+#pragma unroll
+      for (int r = 0; r < RC; ++r) an[r] = wfrag[r][(st + 1) * 64];
+    }
+    const unsigned c = unsigned(st * 4 + grp);
+    const int tap = cpt == 1 ? int(c) : int(__umulhi(c, a.cmagic));
+    const int ch = int(c) - tap * cpt;
+    const bool tin = tap < 9;
+    const int ky = (tap * 11) >> 5, kx = tap - ky * 3;  // tap / 3 for tap < 9
+    h8 bf[RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int ry = (wave * RP + p) * S + ky, cx = col * S + kx;
+      bf[p] = tin ? stile[(ry * CI + cx) * cpt + ch] : zero;
+    }
+#pragma unroll
+    for (int r = 0; r < RC; ++r)
+#pragma unroll
+      for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+  }
+  // epilogue: bias, SiLU, optional residual, fp16 NHWC store
+  const int ox = ox0 + col;
+  if (ox >= a.Wo) return;
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co0 = (cot0 + r) * 16 + grp * 4;
+    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int oy = oy0 + wave * RP + p;
+      if (oy >= a.Ho) continue;
+      const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float tt = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(tt) : tt;
+      }
+      _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
+      if (a.res) {
+        const _Float16* ro = a.res + pix * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          const h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] += (float)ro[j];
+        }
+      }
+      if (a.vec_ok && co0 + 3 < a.cout) {
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) yo[j] = (_Float16)v[j];
+      }
+    }
+  }
+}
+
+static size_t small_tile_lds(int stride, int rp, int cin) {
+  const int th = 4 * rp, ri = (th - 1) * stride + 3, ci = 15 * stride + 3;
+  return size_t(ri) * ci * (cin / 8) * 16;
 }
 
 // ============================================================================ depthwise 3x3
@@ -1094,6 +1347,18 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int rp : {1, 2, 4})
       if (n < cap) out[n++] = rc | (rp << 4);
   }
+  if (d.k == 1 && d.cin % 32 == 0 && stream_nsm(d.cin / 32) > 0)  // streaming 1x1: 0x300 | rc | rp << 4
+    for (int rc : {1, 2, 4}) {
+      if (det_box ? rc != 4 : (rc > 1 && (rc >> 1) >= cotiles)) continue;
+      for (int rp : {1, 2})
+        if (n < cap && stream_ok(stream_nsm(d.cin / 32), rc, rp)) out[n++] = 0x300 | rc | (rp << 4);
+    }
+  if (d.k == 3 && d.cin % 32 != 0 && d.cin <= 64 && d.up == 0 && !det_box)  // small-cin LDS tile: 0x200 | ..
+    for (int rc : {1, 2, 4}) {
+      if (rc > 1 && (rc >> 1) >= cotiles) continue;
+      for (int rp : {1, 2, 4})
+        if (n < cap && small_tile_lds(d.stride, rp, d.cin) <= 64 * 1024) out[n++] = 0x200 | rc | (rp << 4);
+    }
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel, coded 0x100 | rc | rp << 4
     for (int rc : {1, 2, 4}) {
       if (rc > 1 && (rc >> 1) >= cotiles) continue;
@@ -1121,6 +1386,40 @@ static void launch_tile3_s(const ConvArgs& a, int rc, int rp, dim3 grid, hipStre
     launch_tile3_rc<S, 2>(a, rp, grid, s);
   else
     launch_tile3_rc<S, 4>(a, rp, grid, s);
+}
+
+template <int S, int RC>
+static void launch_small3_rc(const ConvArgs& a, int rp, dim3 grid, size_t lds, hipStream_t s) {
+  if (rp == 1)
+    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 1>), grid, dim3(256), lds, s, a);
+  else if (rp == 2)
+    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 2>), grid, dim3(256), lds, s, a);
+  else
+    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 4>), grid, dim3(256), lds, s, a);
+}
+
+template <int S>
+static void launch_small3_s(const ConvArgs& a, int rc, int rp, dim3 grid, size_t lds, hipStream_t s) {
+  if (rc == 1)
+    launch_small3_rc<S, 1>(a, rp, grid, lds, s);
+  else if (rc == 2)
+    launch_small3_rc<S, 2>(a, rp, grid, lds, s);
+  else
+    launch_small3_rc<S, 4>(a, rp, grid, lds, s);
+}
+
+static int launch_small3(const ConvArgs& a, int rc, int rp, int stride, int n, hipStream_t s) {
+  const int th = 4 * rp;
+  const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
+  FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 small tile: grid too large");
+  const size_t lds = small_tile_lds(stride, rp, a.cin);
+  FCE_CHECK(lds <= 64 * 1024, "conv 3x3 small tile: LDS tile too large");
+  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + rc - 1) / rc));
+  if (stride == 1)
+    launch_small3_s<1>(a, rc, rp, grid, lds, s);
+  else
+    launch_small3_s<2>(a, rc, rp, grid, lds, s);
+  return launch_status("conv3x3_tile_small_kernel");
 }
 
 static int launch_tile3(const ConvArgs& a, int rc, int rp, int stride, int n, hipStream_t s) {
@@ -1282,6 +1581,21 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_stride = det ? det->stride : 0.f;
   const bool fast = d.cin % 32 == 0;
   int rc, rp;
+  if (tile >= 0x300) {  // streaming 1x1 kernel
+    rc = tile & 15;
+    rp = (tile >> 4) & 15;
+    FCE_CHECK(d.k == 1 && fast && (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2), "conv: bad stream hint");
+    if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
+    return launch_stream(a, out_kind, rc, rp, s);
+  }
+  if (tile >= 0x200) {  // small-cin LDS tile 3x3 kernel
+    rc = tile & 15;
+    rp = (tile >> 4) & 15;
+    FCE_CHECK(d.k == 3 && !fast && d.cin <= 64 && out_kind == OUT_F16 && d.up == 0 && (rc == 1 || rc == 2 || rc == 4) &&
+                  (rp == 1 || rp == 2 || rp == 4),
+              "conv: bad small-cin LDS-tile hint");
+    return launch_small3(a, rc, rp, d.stride, x.n, s);
+  }
   if (tile >= 0x100) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;

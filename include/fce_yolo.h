@@ -94,6 +94,14 @@ int fce_conv_pack_weights(const fce_conv_desc* d, const float* w_oihw, void* pac
 int fce_conv2d(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
                const fce_tensor* residual, const fce_tensor* y, void* stream);
 
+/* Kernel variants of a conv (register tiles / LDS-tiled kernels / depthwise variants) for input width
+ * in_w; every variant computes each output with the same summation order, so all give bitwise the
+ * same result — the executor times them at plan and keeps the fastest.  Returns the count (<= cap). */
+int fce_conv_variants(const fce_conv_desc* d, int in_w, int* codes, int cap);
+/* fce_conv2d with an explicit variant code from fce_conv_variants (-1 = heuristic). */
+int fce_conv2d_variant(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
+                       const fce_tensor* residual, const fce_tensor* y, int variant, void* stream);
+
 /* Detect tail fused into the last 1x1 conv of a branch (head.py:149-167): part 0 = box branch
  * (4*reg_max logits -> DFL expectation -> xywh * stride into pred rows 0..3), part 1 = cls branch
  * (nc logits -> sigmoid into pred rows 4..).  pred: (N, 4+nc, anchors) fp32; this level's anchors
@@ -205,6 +213,10 @@ int fce_net_num_ops(const fce_net* net);
 /* name (kernel family), algorithmic bytes and flops of op i at the planned size */
 int fce_net_op_info(const fce_net* net, int i, char* name, int name_cap, double* bytes, double* flops);
 int fce_net_buffer(const fce_net* net, int id, fce_tensor* out);
+/* kernel variant code the plan-time autotune chose for op i (-1 = heuristic / not tunable) */
+int fce_net_op_variant(const fce_net* net, int i);
+/* k-th autotune measurement of the last plan: op index, variant code, ms per run; returns 0 past the end */
+int fce_net_tune_record(const fce_net* net, int k, int* op, int* code, float* ms);
 
 #ifdef __cplusplus
 }

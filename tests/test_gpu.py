@@ -8,6 +8,7 @@ Tolerances (fp16 storage, fp32 accumulate, fp32 decode — Q11):
   * NMS:           kept anchor indices and (k, 6) rows bit-exact vs the reference on the same preds.
 """
 
+import ctypes as C
 import hashlib
 
 import numpy as np
@@ -254,3 +255,50 @@ def test_pipeline_overlap_matches_sequential(device):
         d, k = pipe2.results(pipe2.submit(x))
         for b in range(B):
             assert torch.equal(d[b], seq[i][0][b]) and torch.equal(k[b], seq[i][1][b]), (i, b)
+
+
+CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
+    (8, 8, 3, 1, 37, 45, True), (16, 32, 3, 2, 40, 50, False), (8, 16, 3, 1, 33, 20, False),
+    (48, 64, 3, 1, 21, 35, False), (24, 40, 3, 2, 19, 31, False), (64, 64, 3, 1, 40, 40, True),
+    (32, 16, 1, 1, 30, 30, False), (96, 80, 3, 2, 23, 29, False), (128, 64, 3, 1, 20, 20, False),
+    (128, 64, 1, 1, 25, 27, True), (256, 40, 1, 1, 16, 24, False), (96, 48, 1, 1, 41, 17, False),
+    (64, 128, 1, 1, 30, 40, False),
+]
+
+
+@pytest.mark.parametrize("case", CONV_VARIANT_CASES)
+def test_conv_every_variant_bitwise_and_parity(case, device):
+    """Every kernel variant the executor may autotune to (register tiles, LDS-tile kernels) gives the
+    bit-identical result, and that result matches the fp64 reference within the per-op tolerance."""
+    cin, cout, k, stride, H, W, with_res = case
+    g = torch.Generator().manual_seed(cin * 1000 + cout)
+    w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(2, cin, H, W, generator=g).half()
+    desc = N.ConvDesc(cin, cout, k, stride, 1, N.ACT_SILU, 0, 0, None, 0, 0)
+    wp = M.pack_conv(desc, w, device)
+    bd = b.float().to(device)
+    xd = x.to(device).permute(0, 2, 3, 1).contiguous()
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, k // 2)
+    res = None
+    if with_res:
+        r = torch.randn(2, cout, Ho, Wo, generator=g).half()
+        res = r.to(device).permute(0, 2, 3, 1).contiguous()
+    ref = torch.nn.functional.silu(ref) + (r.double() if with_res else 0)
+    xt = N.Tensor(xd.data_ptr(), N.F16, N.NHWC, 2, cin, H, W, cin, 0)
+    rt = N.Tensor(res.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout, 0) if with_res else None
+    codes = (C.c_int * 64)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 64)
+    assert nv >= 2
+    outs = {}
+    for code in [-1] + list(codes[:nv]):
+        y = torch.full((2, Ho, Wo, cout), float("nan"), dtype=torch.float16, device=device)
+        yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout, 0)
+        N.call("fce_conv2d_variant", C.byref(desc), C.byref(xt), wp.data_ptr(), bd.data_ptr(),
+               C.byref(rt) if rt is not None else None, C.byref(yt), code, None)
+        outs[code] = y.permute(0, 3, 1, 2).cpu()
+    base = outs[-1]
+    for code, y in outs.items():
+        assert torch.equal(y, base), hex(code)
+    assert _rel(base, ref) <= 4e-3
