@@ -73,6 +73,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     ap.add_argument("--profile-passes", type=int, default=10, help="per-op HIP-event passes averaged")
+    ap.add_argument("--predict-steps", type=int, default=10,
+                    help="batches of the host-image predict path timed after the main line (0 = skip)")
     return ap.parse_args()
 
 
@@ -86,6 +88,30 @@ def model_cfg(name: str):
         if row[2] == "BiCoordCrossAtt":
             row[3] = [512, 8, 8]
     return d
+
+
+def predict_rate(model, B: int, S: int, dev, steps: int):
+    """Whole predict path from HOST images (not `value`): B decoded 480x640 uint8 BGR numpy images per
+    step -> H2D copy -> device letterbox -> forward -> NMS -> scale_boxes -> per-image results on host."""
+    import numpy as np
+
+    from fce_yolo_amd.predict import Predictor
+
+    pred = Predictor(model, B, S, dev)
+    rng = np.random.default_rng(0)
+    imgs = [rng.integers(0, 256, (480, 640, 3), dtype=np.uint8) for _ in range(B)]
+    for _ in range(2):
+        pred(imgs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pred(imgs)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pred.close()
+    return {"images_per_sec": round(B * steps / el, 2), "ms_per_batch": round(el / steps * 1e3, 3),
+            "source": f"{B} x 480x640 uint8 BGR host numpy images per batch (pageable H2D), device letterbox to "
+                      f"{S}x{S} + forward + NMS + scale_boxes + results to host, {steps} batches"}
 
 
 def cpu_baseline(model_name: str, imgsz: int, seconds: float):
@@ -254,6 +280,8 @@ def main():
     }
     if a.profile_json and rank == 0:
         Path(a.profile_json).write_text(json.dumps([list(p) for p in prof], indent=0))
+    if rank == 0 and world == 1 and a.predict_steps > 0:
+        out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds)
     elif rank == 0:

@@ -94,6 +94,8 @@ _SIGS = {
     "fce_conv_pack_weights": (_I, [_PCD, _P, _P]),
     "fce_conv2d": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _P]),
     "fce_conv_variants": (_I, [_PCD, _I, _P, _I]),
+    "fce_letterbox": (_I, [_P, _I, _P, _I, _I, _I, _P]),
+    "fce_scale_boxes": (_I, [_P, _P, _I, _I, _P, _P]),
     "fce_conv2d_variant": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _I, _P]),
     "fce_conv2d_detect": (_I, [_PCD, _PT, _P, _P, C.POINTER(DetectEpi), _P]),
     "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),

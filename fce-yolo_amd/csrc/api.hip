@@ -41,6 +41,9 @@ size_t nms_ws_bytes(int n, int A, int max_nms);
 int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
         void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
 
+int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
+int scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* sc, hipStream_t s);
+
 static thread_local std::string g_err;
 static thread_local LaunchProbe* g_probe = nullptr;
 LaunchProbe*& probe_slot() { return g_probe; }
@@ -148,6 +151,13 @@ int fce_nms(const float* pred, int n, int nc, int A, float conf, float iou, int 
             void* ws, size_t wsb, float* dets, int64_t* keep, int32_t* counts, void* stream) {
   FCE_CHECK(pred && dets && keep && counts, "fce_nms: null argument");
   FCE_GUARD(return nms(pred, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts, S(stream));)
+}
+int fce_letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad_value, void* stream) {
+  FCE_GUARD(return letterbox(imgs, n, dst, H, W, pad_value, S(stream));)
+}
+int fce_scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* params,
+                    void* stream) {
+  FCE_GUARD(return scale_boxes(dets, counts, n, max_det, params, S(stream));)
 }
 int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
   FCE_CHECK(src && dst, "fce_copy: null argument");

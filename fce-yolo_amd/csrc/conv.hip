@@ -1038,9 +1038,12 @@ template <>
 __device__ __forceinline__ float ld_in<float>(const float* p, int64_t i) {
   return p[i];
 }
+// uint8 network input: the reference preprocess (predictor.py:151-173) computes `im.half() / 255`, i.e.
+// the fp16 rounding of v / 255 — the value the fp16 model sees for every pixel
+__device__ __forceinline__ float u8_to_unit(unsigned v) { return (float)(_Float16)((float)v / 255.0f); }
 template <>
 __device__ __forceinline__ float ld_in<uint8_t>(const uint8_t* p, int64_t i) {
-  return (float)p[i] * (1.0f / 255.0f);
+  return u8_to_unit(p[i]);
 }
 
 template <int COUT, typename T>
@@ -1128,7 +1131,7 @@ struct RawRun {
       const unsigned short h = (unsigned short)(w[e >> 1] >> ((e & 1) * 16));
       return (float)__ushort_as_half(h);
     } else {
-      return (float)((w[e >> 2] >> ((e & 3) * 8)) & 255u) * (1.0f / 255.0f);
+      return u8_to_unit((w[e >> 2] >> ((e & 3) * 8)) & 255u);
     }
   }
 };

@@ -114,6 +114,27 @@ typedef struct fce_detect_epi {
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
                       const fce_detect_epi* e, void* stream);
 
+/* ---------------------------------------------------------------- pre / post processing */
+/* One decoded source image (uint8 HWC BGR, device memory) and its letterbox placement, as computed by
+ * the reference's LetterBox (data/augment.py:1555-1610; auto=False, center=True, scaleup=True). */
+typedef struct fce_letterbox_img {
+  const uint8_t* src;
+  int h0, w0, row_stride;  /* source rows of row_stride bytes */
+  int new_h, new_w;        /* resized (unpadded) size */
+  int top, left;           /* placement on the canvas */
+} fce_letterbox_img;
+/* predictor.py:151-201 preprocess on the device: resize (cv2 INTER_LINEAR u8 semantics), pad with
+ * pad_value, BGR -> RGB; dst = uint8 NCHW (n, 3, H, W), the engine's u8 network input.  imgs: n
+ * descriptors in device memory. */
+int fce_letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad_value, void* stream);
+/* utils/ops.py:102-176 scale_boxes + clip_boxes per image (ratio_pad=None form): for slot k < counts[b]
+ * of dets (n, max_det, 6): xyxy -= (pad_x, pad_y), /= gain, clamped to [0, w0] x [0, h0]. */
+typedef struct fce_box_scale {
+  float gain;
+  int pad_x, pad_y, h0, w0;
+} fce_box_scale;
+int fce_scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* params, void* stream);
+
 /* ---------------------------------------------------------------- pooling / fusion */
 /* SPPF chain: y1 = maxpool_k(x), y2 = maxpool_k(y1), y3 = maxpool_k(y2), stride 1, -inf pad. */
 int fce_maxpool_chain(const fce_tensor* x, const fce_tensor* y1, const fce_tensor* y2, const fce_tensor* y3, int k,
