@@ -128,31 +128,52 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return act == ACT_SILU_ ? v / (1.0f + expf(-v)) : act == ACT_SIGMOID_ ? 1.0f / (1.0f + expf(-v)) : v;
 }
 
-// grid (position tiles, jobs, N); tile of TP positions staged in LDS, and the [K][M] weight matrix
-// too when it fits (wlds): the K-long dot products then run from LDS instead of a chain of L2 loads.
-__global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP, int wlds) {
+// grid (position tiles, jobs, N): a block computes TP positions x all M outputs of one job.  K is
+// walked in chunks of KC: the TP x KC source slice and the KC x M weight slice are staged in LDS with
+// coalesced loads, then every thread accumulates its (position, output) pairs from LDS (consecutive
+// threads = consecutive outputs: conflict-free weight reads, broadcast source reads).
+__global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP, int KC) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const ProjJob& jb = pa.job[blockIdx.y];
   const int n = blockIdx.z;
   const int p0 = blockIdx.x * TP;
   if (p0 >= jb.L) return;
-  const int np = min(TP, jb.L - p0);
-  const float* src = jb.src + (int64_t(n) * jb.L + p0) * jb.K;
-  for (int e = threadIdx.x; e < np * jb.K; e += blockDim.x) sm[e] = src[e];
-  const float* wt = jb.wt;
-  if (wlds) {
-    float* ws = sm + TP * jb.K;
-    for (int e = threadIdx.x; e < jb.K * jb.M; e += blockDim.x) ws[e] = jb.wt[e];
-    wt = ws;
+  const int np = min(TP, jb.L - p0), M = jb.M, K = jb.K;
+  float* ss = sm;              // [TP][KC]
+  float* ws = sm + TP * KC;    // [KC][M]
+  constexpr int OPT = 16;      // outputs per thread (TP * M <= 256 * OPT)
+  float acc[OPT];
+#pragma unroll
+  for (int i = 0; i < OPT; ++i) {
+    const int e = threadIdx.x + i * 256;
+    acc[i] = (e < np * M && jb.b) ? jb.b[e % M] : 0.f;
   }
-  __syncthreads();
-  float* dst = jb.dst + (int64_t(n) * jb.L + p0) * jb.M;
-  for (int e = threadIdx.x; e < np * jb.M; e += blockDim.x) {
-    const int i = e / jb.M, m = e - (e / jb.M) * jb.M;
-    const float* s = sm + i * jb.K;
-    float acc = jb.b ? jb.b[m] : 0.f;
-    for (int c = 0; c < jb.K; ++c) acc += s[c] * wt[c * jb.M + m];
-    dst[e] = act_f(acc, jb.act);
+  const float* src = jb.src + (int64_t(n) * jb.L + p0) * K;
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    const int kc = min(KC, K - k0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < np * kc; e += 256) {
+      const int i = e / kc, c = e - i * kc;
+      ss[i * KC + c] = src[int64_t(i) * K + k0 + c];
+    }
+    for (int e = threadIdx.x; e < kc * M; e += 256) ws[e] = jb.wt[int64_t(k0) * M + e];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < OPT; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e >= np * M) break;
+      const int pi = e / M, m = e - pi * M;
+      const float* sp = ss + pi * KC;
+      float t = acc[i];
+      for (int c = 0; c < kc; ++c) t += sp[c] * ws[c * M + m];
+      acc[i] = t;
+    }
+  }
+  float* dst = jb.dst + (int64_t(n) * jb.L + p0) * M;
+#pragma unroll
+  for (int i = 0; i < OPT; ++i) {
+    const int e = threadIdx.x + i * 256;
+    if (e < np * M) dst[e] = act_f(acc[i], jb.act);
   }
 }
 
@@ -237,6 +258,90 @@ __global__ __launch_bounds__(256) void coord_attend_kernel(AttArgs a) {
   }
 }
 
+// Lane-group version: a group of KG = 16 lanes owns one (query, head) and splits the keys (lane g takes
+// keys g, g + 16, ...), each lane an online softmax over its keys; the 16 partial (max, sum, acc) states
+// are merged with 4 xor-shuffle rounds.  Blocks loop over query tiles of QT = 16 / heads queries (x
+// heads = 16 groups = 256 threads); K/V of the (image, branch) are staged in LDS once per block.  The
+// serial chain per lane is Lk / 16 keys instead of Lk.
+constexpr int KG = 16;
+
+template <int DH>
+__global__ __launch_bounds__(256) void coord_attend_groups_kernel(AttArgs a, int qper) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const AttJob& jb = a.job[blockIdx.y];
+  const int n = blockIdx.z;
+  const int mid = a.mid, Lk = jb.Lk, heads = a.heads;
+  const int QT = KG / heads;  // queries per tile (16 groups per block)
+  const int q0 = blockIdx.x * qper;
+  if (q0 >= jb.Lq) return;
+  const int q1 = min(jb.Lq, q0 + qper), nq = q1 - q0;
+  // K / V rows at an odd float stride: the 16 lanes of a group read 16 different keys at once, and an
+  // even stride (mid = 16 / 64) would put them in 4..16 of the same LDS banks
+  const int ld = mid | 1;
+  float* ks = sm;              // Lk*ld
+  float* vs = ks + Lk * ld;    // Lk*ld
+  float* ys = vs + Lk * ld;    // qper*mid: attention outputs of all the block's queries
+  float* qs = ys + qper * mid;  // qper*mid: the block's queries
+  const float* kg = jb.k + int64_t(n) * Lk * mid;
+  const float* vg = jb.v + int64_t(n) * Lk * mid;
+  for (int e = threadIdx.x; e < Lk * mid; e += blockDim.x) {
+    const int j = e / mid, c = e - j * mid;
+    ks[j * ld + c] = kg[e];
+    vs[j * ld + c] = vg[e];
+  }
+  const float* qg0 = jb.q + (int64_t(n) * jb.Lq + q0) * mid;
+  for (int e = threadIdx.x; e < nq * mid; e += blockDim.x) qs[e] = qg0[e];
+  __syncthreads();
+  const int grp = threadIdx.x / KG, gl = threadIdx.x % KG;
+  const int qi = grp / heads, hd = grp - qi * heads;  // group -> (query in tile, head)
+  for (int t0 = 0; t0 < nq; t0 += QT) {
+    const int il = t0 + qi;
+    if (qi < QT && il < nq) {
+      const float* qg = qs + il * mid + hd * DH;
+      float q[DH], acc[DH];
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        q[d] = qg[d];
+        acc[d] = 0.f;
+      }
+      float m = -INFINITY, l = 0.f;
+      for (int j = gl; j < Lk; j += KG) {
+        const float* kj = ks + j * ld + hd * DH;
+        float sc = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) sc += q[d] * kj[d];
+        sc *= a.scale;
+        const float mn = fmaxf(m, sc);
+        const float corr = expf(m - mn), pj = expf(sc - mn);
+        l = l * corr + pj;
+        const float* vj = vs + j * ld + hd * DH;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc[d] = acc[d] * corr + pj * vj[d];
+        m = mn;
+      }
+#pragma unroll
+      for (int off = 1; off < KG; off <<= 1) {  // merge the 16 partial softmax states of the group
+        const float mo = __shfl_xor(m, off), lo = __shfl_xor(l, off);
+        const float mn = fmaxf(m, mo);
+        const float ca = m == -INFINITY ? 0.f : expf(m - mn), cb = mo == -INFINITY ? 0.f : expf(mo - mn);
+        l = l * ca + lo * cb;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc[d] = acc[d] * ca + __shfl_xor(acc[d], off) * cb;
+        m = mn;
+      }
+      if (gl == 0) {
+        const float inv = 1.0f / l;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) ys[il * mid + hd * DH + d] = acc[d] * inv;
+      }
+    }
+  }
+  __syncthreads();
+  // attention outputs [Lq][mid] (the output projection runs as a coord_proj job)
+  float* dst = jb.dst + (int64_t(n) * jb.Lq + q0) * mid;
+  for (int e = threadIdx.x; e < nq * mid; e += blockDim.x) dst[e] = ys[e];
+}
+
 // ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
@@ -282,21 +387,25 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
 // ---------------------------------------------------------------------------- host
 static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
   ProjArgs pa;
-  int maxL = 1, maxK = 1;
+  int maxL = 1, maxM = 1, maxK = 1;
   for (int i = 0; i < nj; ++i) {
     pa.job[i] = jobs[i];
     maxL = std::max(maxL, jobs[i].L);
+    maxM = std::max(maxM, jobs[i].M);
     maxK = std::max(maxK, jobs[i].K);
   }
-  const int TP = std::max(1, std::min(16, 8192 / maxK));
-  int maxKM = 0;
-  for (int i = 0; i < nj; ++i) maxKM = std::max(maxKM, jobs[i].K * jobs[i].M);
-  const int wlds = (size_t(TP) * maxK + maxKM) * sizeof(float) <= 64 * 1024;
+  FCE_CHECK(maxM <= 256 * 16, "coord projection: too many outputs");
+  const int TP = std::max(1, std::min(16, 256 * 16 / maxM));                       // positions per block
+  const int KC = std::max(1, std::min({maxK, 256, (8192 - TP * 64) / maxM}));      // <= 32 KiB of weights
+  const size_t shm = (size_t(TP) * KC + size_t(KC) * maxM) * sizeof(float);
   dim3 grid((maxL + TP - 1) / TP, nj, N);
-  FCE_LAUNCH(coord_proj_kernel, grid, dim3(256), (size_t(TP) * maxK + (wlds ? maxKM : 0)) * sizeof(float), s,
-                     pa, TP, wlds);
+  FCE_LAUNCH(coord_proj_kernel, grid, dim3(256), shm, s, pa, TP, KC);
   return launch_status("coord_proj_kernel");
 }
+
+// heads dividing 16: lane-group kernel writing the attention outputs (the caller then runs the output
+// projection as a coord_proj job); otherwise the per-thread kernel with the projection fused
+static bool attend_grouped(const fce_coord_desc& d) { return d.heads <= KG && KG % d.heads == 0; }
 
 static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, hipStream_t s) {
   AttArgs a;
@@ -304,7 +413,6 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
   a.heads = d.heads;
   a.oup = d.oup;
   a.scale = d.scale;
-  a.QT = std::max(1, 256 / d.heads);
   int maxLq = 1, maxLk = 1;
   for (int i = 0; i < nj; ++i) {
     a.job[i] = jobs[i];
@@ -312,21 +420,37 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
     maxLk = std::max(maxLk, jobs[i].Lk);
   }
   constexpr size_t kMaxLds = 160 * 1024;  // gfx950 LDS per workgroup (opted in below)
-  size_t shm = (size_t(2) * maxLk * d.mid + size_t(a.QT) * d.mid) * sizeof(float);
+  const bool groups = attend_grouped(d);
+  a.QT = groups ? KG / d.heads : std::max(1, 256 / d.heads);
+  // group kernel: ~8 blocks per (image, branch), each looping over its query tiles (K/V staged once
+  // per block) and projecting all of its <= 32 queries at the end
+  const int tiles = (maxLq + a.QT - 1) / a.QT;
+  const int per = std::max(1, std::min((tiles + 7) / 8, 32 / std::max(1, a.QT)));
+  const int qper = per * a.QT;
+  size_t shm = (size_t(2) * maxLk * (groups ? (d.mid | 1) : d.mid) + size_t(groups ? 2 * qper : a.QT) * d.mid) *
+               sizeof(float);
   if (shm > kMaxLds) return fail(FCE_ERR_UNSUPPORTED, "coord attention: K/V do not fit in LDS");
-  a.wlds = shm + size_t(d.mid) * d.oup * sizeof(float) <= kMaxLds;
+  a.wlds = !groups && shm + size_t(d.mid) * d.oup * sizeof(float) <= kMaxLds;
   if (a.wlds) shm += size_t(d.mid) * d.oup * sizeof(float);
-  dim3 grid((maxLq + a.QT - 1) / a.QT, nj, N);
+  dim3 grid = groups ? dim3((maxLq + qper - 1) / qper, nj, N) : dim3((maxLq + a.QT - 1) / a.QT, nj, N);
   const int dh = d.mid / d.heads;
   switch (dh) {
-#define ATT(DH)                                                                                         \
-  case DH: {                                                                                            \
-    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&coord_attend_kernel<DH>), \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,         \
-                                                    int(kMaxLds)) == hipSuccess;                        \
-    if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord attention: cannot opt in to >64 KiB LDS"); \
-    FCE_LAUNCH(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a);                            \
-    break;                                                                                              \
+#define ATT(DH)                                                                                          \
+  case DH: {                                                                                             \
+    if (groups) {                                                                                        \
+      static const bool lds_ok = hipFuncSetAttribute(                                                    \
+          reinterpret_cast<const void*>(&coord_attend_groups_kernel<DH>),                                \
+          hipFuncAttributeMaxDynamicSharedMemorySize, int(kMaxLds)) == hipSuccess;                       \
+      if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord attention: cannot opt in to >64 KiB LDS"); \
+      FCE_LAUNCH(coord_attend_groups_kernel<DH>, grid, dim3(256), shm, s, a, qper);                      \
+    } else {                                                                                             \
+      static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&coord_attend_kernel<DH>), \
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                                                      int(kMaxLds)) == hipSuccess;                       \
+      if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord attention: cannot opt in to >64 KiB LDS"); \
+      FCE_LAUNCH(coord_attend_kernel<DH>, grid, dim3(256), shm, s, a);                                   \
+    }                                                                                                    \
+    break;                                                                                               \
   }
     ATT(1) ATT(2) ATT(3) ATT(4) ATT(5) ATT(6) ATT(7) ATT(8) ATT(10) ATT(12) ATT(16) ATT(20) ATT(24) ATT(32)
     ATT(48) ATT(64)
@@ -370,9 +494,16 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
         {w.xh, d.w[5], d.b[5], w.buf[5], H, C, mid, ACT_NONE_},  // v_w  <- x_h
     };
     if ((st = launch_proj(pj, 6, N, s))) return st;
-    AttJob aj[2] = {{w.buf[0], w.buf[1], w.buf[2], d.w[6], d.b[6], w.g1, H, W, ACT_NONE_},
-                    {w.buf[3], w.buf[4], w.buf[5], d.w[7], d.b[7], w.g2, W, H, ACT_NONE_}};
+    const bool grp = attend_grouped(d);  // grouped: attention outputs overwrite the queries (each block
+                                         // writes exactly the rows it read), then out_h / out_w jobs
+    AttJob aj[2] = {{w.buf[0], w.buf[1], w.buf[2], d.w[6], d.b[6], grp ? w.buf[0] : w.g1, H, W, ACT_NONE_},
+                    {w.buf[3], w.buf[4], w.buf[5], d.w[7], d.b[7], grp ? w.buf[3] : w.g2, W, H, ACT_NONE_}};
     if ((st = launch_attend(aj, 2, N, d, s))) return st;
+    if (grp) {
+      ProjJob po[2] = {{w.buf[0], d.w[6], d.b[6], w.g1, H, mid, d.oup, ACT_NONE_},
+                       {w.buf[3], d.w[7], d.b[7], w.g2, W, mid, d.oup, ACT_NONE_}};
+      if ((st = launch_proj(po, 2, N, s))) return st;
+    }
   } else if (kind == 1) {  // CoordAtt: y = SiLU(cv1 [x_h; x_w]); a_h / a_w = sigmoid(cv_h / cv_w)
     ProjJob p1[2] = {{w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_SILU_},
                      {w.xw, d.w[0], d.b[0], w.buf[1], W, C, mid, ACT_SILU_}};
@@ -388,8 +519,13 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
                      {w.buf[1], d.w[2], d.b[2], w.buf[3], W, mid, mid, ACT_NONE_},
                      {w.buf[1], d.w[3], d.b[3], w.buf[4], W, mid, mid, ACT_NONE_}};
     if ((st = launch_proj(p2, 3, N, s))) return st;
-    AttJob aj[1] = {{w.buf[2], w.buf[3], w.buf[4], d.w[4], d.b[4], w.g1, H, W, ACT_SIGMOID_}};
+    const bool grp = attend_grouped(d);
+    AttJob aj[1] = {{w.buf[2], w.buf[3], w.buf[4], d.w[4], d.b[4], grp ? w.buf[2] : w.g1, H, W, ACT_SIGMOID_}};
     if ((st = launch_attend(aj, 1, N, d, s))) return st;
+    if (grp) {
+      ProjJob po[1] = {{w.buf[2], d.w[4], d.b[4], w.g1, H, mid, d.oup, ACT_SIGMOID_}};
+      if ((st = launch_proj(po, 1, N, s))) return st;
+    }
   }
   // identity branch (1x1 conv with bias, no act) written into y first, then gated in place
   const _Float16* src = xp;
