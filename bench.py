@@ -150,10 +150,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
+    local = local % max(1, torch.cuda.device_count())  # (rehearsals with more ranks than GPUs)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FCE_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     model = DetectionModel(model_cfg(a.model))
     if rank == 0:

@@ -33,9 +33,22 @@ def shard_range(total: int, world: int, rank: int, batch_size: int) -> tuple[int
 
 @torch.no_grad()
 def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
-    """Every parameter and buffer of `module` := rank `src`'s (same architecture on all ranks)."""
-    for t in list(module.parameters()) + list(module.buffers()):
-        dist.broadcast(t.data, src=src)
+    """Every parameter and buffer of `module` := rank `src`'s (same architecture on all ranks).
+
+    Bucketed: the tensors of each dtype are flattened into one buffer and sent with ONE broadcast
+    (a few large collectives over xGMI instead of one per tensor), then copied back."""
+    tensors = [t.data for t in list(module.parameters()) + list(module.buffers())]
+    by_dtype: dict = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.broadcast(flat, src=src)
+        off = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n
 
 
 def gather_detections(dets: torch.Tensor, keep: torch.Tensor, counts: torch.Tensor):
