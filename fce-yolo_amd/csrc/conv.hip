@@ -40,8 +40,14 @@ static DenseGeom dense_geom(const fce_conv_desc& d) {
 static bool is_stem(const fce_conv_desc& d) { return d.groups == 1 && d.cin <= 4; }
 static bool is_dw(const fce_conv_desc& d) { return d.groups > 1; }
 
+// 3x3 stems with cin * 9 <= 32 also carry one MFMA K-step of fp16 fragments (k = ci * 9 + tap, zero
+// padded to 32) per 16-cout tile after the fp32 table: the stem_mfma_kernel's A operand
+static bool stem_mfma_ok(const fce_conv_desc& d) { return d.k == 3 && d.cin * 9 <= 32 && d.cout <= 64; }
+static size_t stem_fp32_bytes(const fce_conv_desc& d) { return size_t(d.cin) * d.k * d.k * d.cout * sizeof(float); }
+
 size_t conv_weight_bytes(const fce_conv_desc& d) {
-  if (is_stem(d)) return size_t(d.cin) * d.k * d.k * d.cout * sizeof(float);  // [cin*k*k][cout] fp32
+  if (is_stem(d))  // [cin*k*k][cout] fp32 (+ MFMA fragments)
+    return stem_fp32_bytes(d) + (stem_mfma_ok(d) ? size_t((d.cout + 15) / 16) * 64 * 8 * sizeof(_Float16) : 0);
   if (is_dw(d)) return size_t(d.k) * d.k * d.cin * sizeof(float);             // [k*k][c] fp32
   DenseGeom g = dense_geom(d);
   return size_t(g.cotiles) * g.nalloc * 64 * 8 * sizeof(_Float16);
@@ -54,6 +60,15 @@ int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
     for (int co = 0; co < d.cout; ++co)
       for (int ci = 0; ci < d.cin; ++ci)
         for (int t = 0; t < kk; ++t) o[(ci * kk + t) * d.cout + co] = w[(co * d.cin + ci) * kk + t];
+    if (stem_mfma_ok(d)) {  // lane l of tile ct: cout ct*16 + (l & 15), k = 8 (l >> 4) + j
+      _Float16* f = reinterpret_cast<_Float16*>(static_cast<char*>(out) + stem_fp32_bytes(d));
+      for (int ct = 0; ct < (d.cout + 15) / 16; ++ct)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int co = ct * 16 + (l & 15), kq = 8 * (l >> 4) + j;
+            f[(ct * 64 + l) * 8 + j] = (_Float16)((co < d.cout && kq < d.cin * 9) ? w[co * d.cin * 9 + kq] : 0.f);
+          }
+    }
     return FCE_OK;
   }
   if (is_dw(d)) {  // [t][c]
@@ -1246,6 +1261,88 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
   }
 }
 
+// 3x3 stride-2 stem on MFMA (3 -> <= 64 channels; k = ci * 9 + tap fits one 32-deep K-step).  A block
+// takes SR output rows of one image: the 2 SR + 1 input rows of all channels are staged in LDS as fp16
+// (the network's input type; f32 inputs are rounded, u8 inputs become fp16(v / 255) as im.half() / 255
+// does) with 16-byte loads and a 16-byte zero pad each side; each wave then builds, per 16-pixel fragment, its B operand by
+// gathering the 8 (ci, ky, kx) values of its lane group from LDS and runs RC MFMAs (16 couts each).
+// Lane (col, grp) of D holds couts 4 grp .. of pixel col: 8-byte stores, a fragment's 16 pixels x
+// RC*16 couts contiguous in NHWC.  fp16 weights, fp32 accumulation, like every other conv here.
+template <typename T, int RC>
+__global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float16* wfr) {
+  constexpr int SR = 4;                 // output rows per block
+  constexpr int IR = 2 * SR + 1;        // staged input rows
+  extern __shared__ __attribute__((aligned(16))) _Float16 ssm[];  // [C][IR][8 + W + 8]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int rows = (a.Ho + SR - 1) / SR;
+  const int n = blockIdx.x / rows, oy0 = (blockIdx.x - n * rows) * SR;
+  const int WP = a.W + 16;  // 16-byte zero pads left and right keep every staged chunk aligned
+  const int CW = WP / 8;    // 16-byte chunks per staged row
+  const T* x = static_cast<const T*>(a.x);
+  for (int e = threadIdx.x; e < a.C * IR * CW; e += 256) {
+    const int cr = e / CW, q = e - cr * CW;
+    const int ci = cr / IR, r = cr - ci * IR;
+    const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
+    h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W) {
+      const T* src = x + ((int64_t(n) * a.C + ci) * a.H + iy) * a.W + ix0;
+      RawRun<T, 8> run;
+      run.load(src);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (_Float16)run.get(j);
+    }
+    *reinterpret_cast<h8*>(ssm + cr * WP + q * 8) = v;
+  }
+  // this lane's 8 k values: (ci, ky, kx) -> LDS offset relative to the pixel's window origin
+  int koff[8];
+  bool kin[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kq = 8 * grp + j, ci = kq / 9, t = kq - ci * 9;
+    kin[j] = kq < a.C * 9;
+    koff[j] = kin[j] ? (ci * IR + t / 3) * WP + (t % 3) : 0;  // staged col of ix = 2 ox - 1 + kx is 2 ox + 7 + kx
+  }
+  h8 af[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) af[r] = reinterpret_cast<const h8*>(wfr)[r * 64 + lane];
+  float bz[RC][4];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = r * 16 + grp * 4 + j;
+      bz[r][j] = co < a.cout ? a.bias[co] : 0.f;
+    }
+  __syncthreads();
+  const int fpr = (a.Wo + 15) / 16;  // fragments per output row
+  for (int f = wave; f < SR * fpr; f += 4) {
+    const int rr = f / fpr, fx = f - rr * fpr;
+    const int oy = oy0 + rr;
+    if (oy >= a.Ho) break;
+    const int ox = fx * 16 + col;
+    const int base = (2 * rr) * WP + 2 * min(ox, a.Wo - 1) + 7;  // window origin: staged row 2 rr, col 2 ox + 7
+    h8 b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = kin[j] ? ssm[base + koff[j]] : (_Float16)0.f;
+    _Float16* yo = a.y + ((int64_t(n) * a.Ho + oy) * a.Wo + ox) * a.ycs;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], b, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int co0 = r * 16 + grp * 4;
+      if (ox < a.Wo && co0 < a.cout) {
+        h4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float t = d[j] + bz[r][j];
+          o[j] = (_Float16)(a.act ? silu(t) : t);
+        }
+        *reinterpret_cast<h4*>(yo + co0) = o;
+      }
+    }
+  }
+}
+
 // ============================================================================ dispatch
 static int grid_cap(int64_t blocks) { return int(blocks < 65535 * 16 ? blocks : 65535 * 16); }
 
@@ -1461,6 +1558,37 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     FCE_CHECK(coutT > 0, "stem conv: cout > 96 unsupported");
     const size_t shm = size_t(x.c) * d.k * d.k * coutT * sizeof(float);
     const int PX = coutT <= 32 ? 2 : 1;  // measured: PX 2 beats 4 (occupancy) and 1 (reuse) at cout 16
+    const char* sv = getenv("FCE_STEM_VALU");  // diagnostics: the fp32 VALU stem instead of MFMA
+    if (stem_mfma_ok(d) && d.stride == 2 && x.c == d.cin && d.cout % 16 == 0 && x.w % 8 == 0 &&
+        size_t(x.c) * 9 * (x.w + 16) * 2 <= 64 * 1024 && !(sv && atoi(sv))) {
+      const size_t lds = size_t(x.c) * 9 * (x.w + 16) * sizeof(_Float16);
+      FCE_CHECK(lds <= 64 * 1024, "stem conv: input rows do not fit in LDS");
+      const int64_t blocks2 = int64_t(x.n) * ((Ho + 3) / 4);
+      FCE_CHECK(blocks2 < (int64_t(1) << 31), "stem conv: input too large");
+      const _Float16* wfr = reinterpret_cast<const _Float16*>(static_cast<const char*>(w) + stem_fp32_bytes(d));
+      const int rc = d.cout / 16;
+#define STEMM(T, RC) FCE_LAUNCH((stem_mfma_kernel<T, RC>), dim3(unsigned(blocks2)), dim3(256), lds, s, a, wfr)
+#define STEMM_T(T)          \
+  do {                      \
+    if (rc == 1)            \
+      STEMM(T, 1);          \
+    else if (rc == 2)       \
+      STEMM(T, 2);          \
+    else if (rc == 3)       \
+      STEMM(T, 3);          \
+    else                    \
+      STEMM(T, 4);          \
+  } while (0)
+      if (x.dtype == FCE_F16)
+        STEMM_T(_Float16);
+      else if (x.dtype == FCE_F32)
+        STEMM_T(float);
+      else
+        STEMM_T(uint8_t);
+#undef STEMM_T
+#undef STEMM
+      return launch_status("stem_mfma_kernel");
+    }
     if (d.k == 3 && d.stride == 2 && x.c == 3 && x.w % (2 * PX) == 0) {
       const int64_t threads = int64_t(x.n) * Ho * ((Wo + PX - 1) / PX);
       FCE_CHECK(threads < (int64_t(1) << 31), "stem conv: input too large");

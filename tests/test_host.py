@@ -136,7 +136,15 @@ def test_dw_and_stem_packing():
     d = N.ConvDesc(3, 16, 3, 2, 1, 1, 0, 0, None, 0, 0)
     out = np.empty(N.lib().fce_conv_weight_bytes(C.byref(d)), np.uint8)
     N.call("fce_conv_pack_weights", C.byref(d), w.ctypes.data, out.ctypes.data)
-    assert np.array_equal(out.view(np.float32).reshape(27, 16), w.reshape(16, 27).T)
+    assert out.size == 27 * 16 * 4 + 64 * 8 * 2  # fp32 table + one MFMA fragment (cout 16)
+    assert np.array_equal(out[:27 * 16 * 4].view(np.float32).reshape(27, 16), w.reshape(16, 27).T)
+    frag = out[27 * 16 * 4:].view(np.float16).reshape(64, 8)  # lane l: cout l & 15, k = 8 (l >> 4) + j
+    ref = np.zeros((64, 8), np.float16)
+    for lane in range(64):
+        for j in range(8):
+            k = 8 * (lane >> 4) + j
+            ref[lane, j] = w[lane & 15].reshape(27)[k] if k < 27 else 0
+    assert np.array_equal(frag, ref)
 
 
 def test_error_path_reports_message():
