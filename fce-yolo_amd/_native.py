@@ -126,6 +126,8 @@ _SIGS = {
     "fce_net_profile": (_I, [_P, _PT, _P, _P, _P, _I, _P]),
     "fce_net_num_ops": (_I, [_P]),
     "fce_net_op_variant": (_I, [_P, _I]),
+    "fce_net_op_variants": (_I, [_P, _I, _P, _I]),
+    "fce_net_set_op_variant": (_I, [_P, _I, _I]),
     "fce_net_tune_record": (_I, [_P, _I, _P, _P, _P]),
     "fce_net_op_info": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fce_net_buffer": (_I, [_P, _I, _PT]),

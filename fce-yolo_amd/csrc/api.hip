@@ -711,9 +711,9 @@ static int autotune(fce_net* net) {
   fce_tensor none{};
   for (OpDesc& op : net->ops) {
     if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
-    int cand[32];
+    int cand[48];
     const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0,
-                                         net->W >> net->bufs[op.in].shift, cand, 32);
+                                         net->W >> net->bufs[op.in].shift, cand, 48);
     if (nc_ <= 1) continue;
     float best_ms = 1e30f;
     int best = -1;
@@ -923,6 +923,27 @@ int fce_net_op_info(const fce_net* net, int i, char* name, int cap, double* byte
 
 int fce_net_op_variant(const fce_net* net, int i) {
   return net && i >= 0 && i < int(net->ops.size()) ? net->ops[i].tile : -1;
+}
+
+int fce_net_op_variants(const fce_net* net, int i, int* codes, int cap) {
+  if (!net || i < 0 || i >= int(net->ops.size()) || !codes || cap <= 0 || net->batch <= 0) return 0;
+  const OpDesc& op = net->ops[i];
+  if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) return 0;
+  return conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0, net->W >> net->bufs[op.in].shift,
+                              codes, cap);
+}
+
+int fce_net_set_op_variant(fce_net* net, int i, int code) {
+  FCE_CHECK(net && i >= 0 && i < int(net->ops.size()) && net->batch > 0, "fce_net_set_op_variant: bad argument");
+  OpDesc& op = net->ops[i];
+  FCE_CHECK((op.kind == OP_CONV && op.in >= 0) || op.kind == OP_CONV_DETECT, "fce_net_set_op_variant: not a conv op");
+  if (code != -1) {
+    int cand[48];
+    const int nc = fce_net_op_variants(net, i, cand, 48);
+    FCE_CHECK(std::find(cand, cand + nc, code) != cand + nc, "fce_net_set_op_variant: not a candidate of this op");
+  }
+  op.tile = code;
+  return FCE_OK;
 }
 
 int fce_net_tune_record(const fce_net* net, int k, int* op, int* code, float* ms) {

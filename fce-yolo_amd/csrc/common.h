@@ -66,6 +66,13 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------- device math
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// An fp32 value pinned in a register.  Without it hipcc fuses a multiply or add with the fp16
+// conversion that follows (v_fma_mix*: one rounding instead of two) in some kernels and not in
+// others, and conv variants that must be bitwise identical differ in the last fp16 bit.
+__device__ __forceinline__ float fpin(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // BiFPN normalised weight (fce_block.py:57-58): relu(w_i) / (sum_j relu(w_j) + 1e-4)

@@ -135,6 +135,7 @@ struct ConvArgs {
   unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
   int gx, gy;               // logical grid: pixel tiles x cout tiles (launched 1-D, see kernel)
   int vec_ok;
+  int stg;                  // LDS-tile 1x1 kernels: fp16 output staged through LDS, 16-byte stores
   // fused Detect tail (OUT_DFL / OUT_CLS): pred (N, 4+nc, A) fp32
   float* pred;
   int det_A, det_a0, det_nc, det_hw, det_w;
@@ -254,29 +255,29 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         if (a.vec_ok && co0 + 3 < a.cout) {
           h4 rv = *reinterpret_cast<const h4*>(ro);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
         } else {
           for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] += (float)ro[j];
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
         }
       }
       if (OUT == OUT_WSTORE) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] *= alpha;
+        for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha);
       }
       if (a.vec_ok && co0 + 3 < a.cout) {
         if (OUT == OUT_ACCUM) {
           h4 pv4 = *reinterpret_cast<const h4*>(yo);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (float)pv4[j] + alpha * v[j];
+          for (int j = 0; j < 4; ++j) v[j] = fpin((float)pv4[j] + fpin(alpha * v[j]));
         }
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
       } else {
         for (int j = 0; j < 4; ++j) {
           if (co0 + j >= a.cout) continue;
           float t = v[j];
-          if (OUT == OUT_ACCUM) t = (float)yo[j] + alpha * t;
-          yo[j] = (_Float16)t;
+          if (OUT == OUT_ACCUM) t = fpin((float)yo[j] + fpin(alpha * t));
+          yo[j] = (_Float16)fpin(t);
         }
       }
     }
@@ -540,6 +541,403 @@ static int launch_stream(const ConvArgs& a0, int out_kind, int rc, int rp, hipSt
   return launch_status("conv1x1_stream_kernel");
 }
 
+// Staged fp16 store for the LDS-tile 1x1 kernels (OUT_F16 / OUT_WSTORE with a.stg): the block's output
+// tile (TPB pixels x CB*16 couts) is assembled in LDS (`ot`, rows of CB*16 halves, 16-byte slot sl of
+// pixel px at sl ^ (px & (2 CB - 1))) and written with 16-byte lane stores, whole pixel rows per 2 CB
+// lanes, instead of 8-byte stores scattered over 16 pixels.  Values are computed exactly as in
+// conv_epilogue (bias, SiLU, residual, BiFPN alpha, then one fp16 rounding): bitwise the same.
+// Caller: every thread of the block, after the last B read of `ot`'s memory (barrier inside).
+template <int RC, int RP, int CB, int TPB, int OUT>
+__device__ __forceinline__ void conv_store_staged(const ConvArgs& a, f4 (&acc)[RC][RP], int pix0, int pw, int cbl0,
+                                                  int wc, int col, int grp, _Float16* ot) {
+  constexpr int ROW = CB * 16, NSL = 2 * CB;
+  const int cotiles = (a.cout + 15) >> 4;
+  float alpha = 1.f;
+  if (OUT == OUT_WSTORE) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int ctl = wc * RC + r;  // local cout tile
+    const int co0 = (cbl0 + ctl) * 16 + grp * 4;
+    if (cbl0 + ctl >= cotiles) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int px = pw + p * 16 + col, pix = pix0 + px;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(t) : t;
+      }
+      if (a.res && pix < a.P) {
+        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          const h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
+        }
+      }
+      if (OUT == OUT_WSTORE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha);
+      }
+      const int sl = ctl * 2 + (grp >> 1);
+      *reinterpret_cast<h4*>(ot + px * ROW + ((sl ^ (px & (NSL - 1))) * 8) + (grp & 1) * 4) =
+          h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+    }
+  }
+  __syncthreads();
+  constexpr int NP = TPB * NSL;  // 16-byte pieces of the tile
+#pragma unroll
+  for (int e0 = 0; e0 < NP; e0 += 256) {
+    const int e = e0 + int(threadIdx.x);
+    if (NP % 256 != 0 && e >= NP) break;
+    const int px = e / NSL, sl = e - px * NSL;
+    const int pix = pix0 + px, co = cbl0 * 16 + sl * 8;
+    if (pix < a.P && co < a.cout)
+      *reinterpret_cast<h8*>(static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co) =
+          *reinterpret_cast<const h8*>(ot + px * ROW + (sl ^ (px & (NSL - 1))) * 8);
+  }
+}
+
+// ============================================================================ 1x1, LDS-staged pixel tiles
+// For 1x1 stride-1 convs (any cin % 8 == 0, optional fused nearest upsampling).  A block (4 waves)
+// owns TPB = WP*RP*16 consecutive output pixels and CB = (4/WP)*RC cout tiles; wave (wc, wp) computes
+// RC cout tiles x RP 16-pixel groups.  Per K chunk of NSC 32-channel steps the block stages its
+// pixels' input rows in LDS with full-line loads (8 lanes = one pixel's 128-byte pair of steps) and
+// every wave reads its B fragments from there, instead of each wave issuing fragment-shaped
+// (16 pixels x 64 B) loads that re-read the input once per cout group.
+// LDS image per pair of steps: [pixel][8 x 16 B]; piece j of pixel p sits in slot j ^ ((p >> 1) & 7).
+// That is conflict-free for the staging ds_write_b128 (8 lanes = the 8 slots of one 128-B row) and
+// for the B-fragment ds_read_b128 (each 16-lane group meets 16 distinct 16-B slots of the bank row).
+// Channels past cin are staged as zeros.  A fragments, K-step contents and the per-output summation
+// order are the implicit-GEMM kernel's, so the results are bitwise identical.
+template <int RC, int RP, int WP, int NSC, int OUT>
+__global__ __launch_bounds__(256) void conv1x1_lds_kernel(ConvArgs a) {
+  constexpr int TPB = WP * RP * 16;
+  constexpr int NPAIR = (NSC + 1) / 2;
+  constexpr int NPC = TPB * NPAIR * 8;  // 16-byte pieces staged per chunk
+  static_assert(NPC % 256 == 0, "whole staging rounds");
+  constexpr int IT = NPC / 256;
+  extern __shared__ __attribute__((aligned(16))) h8 xt[];  // [NPAIR][TPB][8]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / WP, wp = wave - wc * WP;
+  int bx, by;  // XCD-aware order, as conv_mfma_kernel: a pixel tile's cout groups share an XCD's L2
+  {
+    const int total = a.gx * a.gy, b = blockIdx.x;
+    const int per = total >> 3, body = per << 3;
+    const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+    bx = L / a.gy;
+    by = L - bx * a.gy;
+  }
+  const int pix0 = bx * TPB;
+  const int cot0 = (by * (4 / WP) + wc) * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  const h8* wfrag[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int ct = min(cot0 + r, cotiles - 1);
+    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
+  }
+  // staging: piece e = threadIdx.x + 256 i -> (pixel p = e / (8 NPAIR), pair q, piece j): a pixel's
+  // chunk is contiguous in global memory, so consecutive lanes read consecutive 16-byte pieces
+  int64_t soff[IT];
+  int spos[IT], sch[IT];
+  bool spv[IT];
+  const int hw = a.Ho * a.Wo;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int j = e & 7, rest = e >> 3;
+    const int p = rest / NPAIR, q = rest - p * NPAIR;
+    const int pix = pix0 + p;
+    spv[i] = pix < a.P;
+    const int pc = spv[i] ? pix : 0;
+    if (a.up) {
+      const int n = pc / hw, r = pc - n * hw;
+      const int oy = r / a.Wo, ox = r - oy * a.Wo;
+      soff[i] = nhwc_off(n, oy >> a.up, ox >> a.up, a.Hs, a.Ws, a.xcs);
+    } else {
+      soff[i] = int64_t(pc) * a.xcs;
+    }
+    sch[i] = q * 64 + j * 8;
+    spos[i] = (q * TPB + p) * 8 + (j ^ ((p >> 1) & 7));
+  }
+  f4 acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  const int pw = wp * RP * 16;  // this wave's first pixel within the tile
+  for (int k0 = 0; k0 < a.nsteps; k0 += NSC) {
+    if (k0) __syncthreads();  // previous chunk's B reads done
+    h8 af[NSC][RC];           // packed A is zero-padded past nsteps: always in bounds
+#pragma unroll
+    for (int s = 0; s < NSC; ++s)
+#pragma unroll
+      for (int r = 0; r < RC; ++r) af[s][r] = wfrag[r][(k0 + s) * 64];
+    h8 v[IT];
+    const int cbase = k0 * 32;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = cbase + sch[i];
+      const bool ok = spv[i] && c < a.cin;
+      v[i] = *(ok ? reinterpret_cast<const h8*>(a.x + soff[i] + c) : reinterpret_cast<const h8*>(g_zero_line));
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) xt[spos[i]] = v[i];
+    __syncthreads();
+    const int nsc = min(NSC, a.nsteps - k0);
+#pragma unroll
+    for (int s = 0; s < NSC; ++s) {
+      if (s < nsc) {
+        h8 bf[RP];
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int px = pw + p * 16 + col;
+          const int j = (s & 1) * 4 + grp;
+          bf[p] = xt[((s >> 1) * TPB + px) * 8 + (j ^ ((px >> 1) & 7))];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][r], bf[p], acc[r][p], 0, 0, 0);
+      }
+    }
+  }
+  if constexpr (OUT == OUT_F16 || OUT == OUT_WSTORE) {
+    if (a.stg) {
+      __syncthreads();  // every wave's last B read done: the staging image becomes the output tile
+      conv_store_staged<RC, RP, (4 / WP) * RC, TPB, OUT>(a, acc, pix0, pw, by * (4 / WP) * RC, wc, col, grp,
+                                                         reinterpret_cast<_Float16*>(xt));
+      return;
+    }
+  }
+  conv_epilogue<RC, RP, OUT>(a, acc, pix0 + pw, cot0, col, grp);
+}
+
+// Source element offset of output pixel pix of a stride-1 1x1 conv (nearest upsampling folded in).
+__device__ __forceinline__ int64_t conv1x1_src(const ConvArgs& a, int pix) {
+  if (!a.up) return int64_t(pix) * a.xcs;
+  const int hw = a.Ho * a.Wo;
+  const int n = pix / hw, r = pix - n * hw;
+  const int oy = r / a.Wo, ox = r - oy * a.Wo;
+  return nhwc_off(n, oy >> a.up, ox >> a.up, a.Hs, a.Ws, a.xcs);
+}
+
+// 1x1 with the whole K (nsteps <= NSC <= 8) in one LDS image, as a persistent double-buffered ring:
+// the same tile geometry, LDS image and fragment reads as conv1x1_lds_kernel, but each block walks a
+// sequence of pixel tiles and issues the global loads of tile i+1 into registers before it computes
+// and stores tile i, so HBM reads stay in flight through the MFMA and epilogue phases (one barrier per
+// tile).  Block b: XCD b % 8, cout group by, slot; pixel tiles bx = xcd + 8 (slot + k nslot): the gy
+// blocks that read the same pixel tiles sit on one XCD and walk them in step (L2 hits), and a block's
+// cout group never changes, so its A fragments are loaded once.  Bitwise identical to the others.
+template <int RC, int RP, int WP, int NSC, int OUT>
+__global__ __launch_bounds__(256) void conv1x1_ring_kernel(ConvArgs a, int nslot) {
+  constexpr int TPB = WP * RP * 16;
+  constexpr int NPAIR = (NSC + 1) / 2;
+  constexpr int BUF = NPAIR * TPB * 8;  // h8 per LDS buffer
+  static_assert(BUF % 256 == 0, "whole staging rounds");
+  constexpr int IT = BUF / 256;
+  extern __shared__ __attribute__((aligned(16))) h8 xr[];  // [2][NPAIR][TPB][8]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / WP, wp = wave - wc * WP;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int by = loc % a.gy, slot = loc / a.gy;
+  int bx = xcd + 8 * slot;
+  if (bx >= a.gx) return;  // block-uniform
+  const int cot0 = (by * (4 / WP) + wc) * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  h8 af[NSC][RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const h8* wf = reinterpret_cast<const h8*>(a.w) + (size_t(min(cot0 + r, cotiles - 1)) * a.nalloc) * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < NSC; ++s) af[s][r] = wf[s * 64];  // zero-padded past nsteps
+  }
+  auto stage_load = [&](int tile, h8 (&v)[IT]) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int j = e & 7, rest = e >> 3;
+      const int p = rest / NPAIR, q = rest - p * NPAIR;
+      const int pix = tile * TPB + p, c = q * 64 + j * 8;
+      const bool ok = pix < a.P && c < a.cin;
+      v[i] = *(ok ? reinterpret_cast<const h8*>(a.x + conv1x1_src(a, pix) + c)
+                  : reinterpret_cast<const h8*>(g_zero_line));
+    }
+  };
+  auto stage_store = [&](int buf, const h8 (&v)[IT]) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int j = e & 7, rest = e >> 3;
+      const int p = rest / NPAIR, q = rest - p * NPAIR;
+      xr[buf * BUF + (q * TPB + p) * 8 + (j ^ ((p >> 1) & 7))] = v[i];
+    }
+  };
+  const int pw = wp * RP * 16;
+  const int step = 8 * nslot;
+  h8 v[IT];
+  stage_load(bx, v);
+  for (int cur = 0; bx < a.gx; cur ^= 1) {
+    stage_store(cur, v);
+    __syncthreads();
+    const int nbx = bx + step;
+    if (nbx < a.gx) stage_load(nbx, v);
+    f4 acc[RC][RP];
+#pragma unroll
+    for (int r = 0; r < RC; ++r)
+#pragma unroll
+      for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NSC; ++s) {
+      if (s < a.nsteps) {
+        h8 bf[RP];
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int px = pw + p * 16 + col;
+          const int j = (s & 1) * 4 + grp;
+          bf[p] = xr[cur * BUF + ((s >> 1) * TPB + px) * 8 + (j ^ ((px >> 1) & 7))];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][r], bf[p], acc[r][p], 0, 0, 0);
+      }
+    }
+    conv_epilogue<RC, RP, OUT>(a, acc, bx * TPB + pw, cot0, col, grp);
+    bx = nbx;
+  }
+}
+
+// LDS-staged 1x1 configurations, coded 0x400 | rc | rp << 4 | log2(wp) << 12 (0x500 | ..: the ring)
+static bool lds1_cfg_ok(int rc, int rp, int wp) {
+  return (rc == 1 && rp == 4 && wp == 1) || (rc == 2 && rp == 4 && wp == 1) || (rc == 2 && rp == 2 && wp == 2) ||
+         (rc == 1 && rp == 4 && wp == 2) || (rc == 1 && rp == 2 && wp == 4) || (rc == 4 && rp == 1 && wp == 4) ||
+         (rc == 4 && rp == 2 && wp == 4);
+}
+static int lds1_nsc(int nsteps, int rc) {
+  const int cap = rc == 4 ? 4 : 8;
+  return nsteps <= 2 ? 2 : nsteps <= 4 || cap == 4 ? 4 : 8;
+}
+static size_t lds1_bytes(int rp, int wp, int nsc) { return size_t(wp) * rp * 16 * ((nsc + 1) / 2) * 128; }
+static size_t lds1_out_bytes(int rc, int rp, int wp) { return size_t(wp) * rp * 16 * (4 / wp) * rc * 16 * 2; }
+
+template <int RC, int RP, int WP, int NSC>
+static void launch_lds1_o(const ConvArgs& a, int out_kind, dim3 grid, size_t lds, hipStream_t s) {
+#define LDS1_L(O) FCE_LAUNCH((conv1x1_lds_kernel<RC, RP, WP, NSC, O>), grid, dim3(256), lds, s, a)
+  switch (out_kind) {
+    case OUT_F16: LDS1_L(OUT_F16); break;
+    case OUT_F32: LDS1_L(OUT_F32); break;
+    case OUT_WSTORE: LDS1_L(OUT_WSTORE); break;
+    case OUT_CLS: LDS1_L(OUT_CLS); break;
+    case OUT_DFL:
+      if constexpr (RC == 4) LDS1_L(OUT_DFL);
+      break;
+    default: LDS1_L(OUT_ACCUM); break;
+  }
+#undef LDS1_L
+}
+
+template <int RC, int RP, int WP>
+static void launch_lds1_n(const ConvArgs& a, int out_kind, int nsc, dim3 grid, size_t lds, hipStream_t s) {
+  if (nsc == 2)
+    launch_lds1_o<RC, RP, WP, 2>(a, out_kind, grid, lds, s);
+  else if (nsc == 4 || RC == 4)
+    launch_lds1_o<RC, RP, WP, 4>(a, out_kind, grid, lds, s);
+  else
+    launch_lds1_o<RC, RP, WP, (RC == 4 ? 4 : 8)>(a, out_kind, grid, lds, s);
+}
+
+static int ring_nsc(int nsteps) { return nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 6 ? 6 : nsteps <= 8 ? 8 : 0; }
+static bool ring_ok(int nsteps, int rc, int rp, int wp) {
+  const int nsc = ring_nsc(nsteps);
+  return nsc > 0 && lds1_cfg_ok(rc, rp, wp) && nsc * rc <= 16 && 2 * lds1_bytes(rp, wp, nsc) <= 64 * 1024;
+}
+
+template <int RC, int RP, int WP, int NSC>
+static void launch_ring_o(const ConvArgs& a, int out_kind, dim3 grid, size_t lds, int nslot, hipStream_t s) {
+#define RING_L(O) FCE_LAUNCH((conv1x1_ring_kernel<RC, RP, WP, NSC, O>), grid, dim3(256), lds, s, a, nslot)
+  switch (out_kind) {
+    case OUT_F16: RING_L(OUT_F16); break;
+    case OUT_F32: RING_L(OUT_F32); break;
+    case OUT_WSTORE: RING_L(OUT_WSTORE); break;
+    case OUT_CLS: RING_L(OUT_CLS); break;
+    case OUT_DFL:
+      if constexpr (RC == 4) RING_L(OUT_DFL);
+      break;
+    default: RING_L(OUT_ACCUM); break;
+  }
+#undef RING_L
+}
+
+template <int RC, int RP, int WP>
+static bool launch_ring_n(const ConvArgs& a, int out_kind, int nsc, dim3 grid, size_t lds, int nslot, hipStream_t s) {
+  if constexpr (RC * 4 <= 16)
+    if (nsc == 4) return launch_ring_o<RC, RP, WP, 4>(a, out_kind, grid, lds, nslot, s), true;
+  if constexpr (RC * 6 <= 16 && 2 * WP * RP * 16 * 3 * 128 <= 64 * 1024)
+    if (nsc == 6) return launch_ring_o<RC, RP, WP, 6>(a, out_kind, grid, lds, nslot, s), true;
+  if constexpr (RC * 8 <= 16 && 2 * WP * RP * 16 * 4 * 128 <= 64 * 1024)
+    if (nsc == 8) return launch_ring_o<RC, RP, WP, 8>(a, out_kind, grid, lds, nslot, s), true;
+  if (nsc != 2) return false;
+  launch_ring_o<RC, RP, WP, 2>(a, out_kind, grid, lds, nslot, s);
+  return true;
+}
+
+static int launch_ring(const ConvArgs& a0, int out_kind, int rc, int rp, int wp, hipStream_t s) {
+  FCE_CHECK(ring_ok(a0.nsteps, rc, rp, wp), "conv 1x1 ring: bad configuration");
+  ConvArgs a = a0;
+  const int cotiles = (a.cout + 15) / 16, cb = (4 / wp) * rc, tpb = wp * rp * 16;
+  a.gx = (a.P + tpb - 1) / tpb;
+  a.gy = (cotiles + cb - 1) / cb;
+  const int nsc = ring_nsc(a.nsteps);
+  const size_t lds = 2 * lds1_bytes(rp, wp, nsc);
+  const int occ = std::max(1, std::min(4, int((160 * 1024) / lds)));  // blocks per CU the LDS allows
+  const int nslot = std::max(1, std::min((a.gx + 7) / 8, 32 * occ / a.gy));
+  FCE_CHECK(int64_t(8) * a.gy * nslot < (int64_t(1) << 31), "conv 1x1 ring: grid too large");
+  const dim3 grid(unsigned(8 * a.gy * nslot));
+  bool ok;
+  if (rc == 1 && rp == 4 && wp == 1) ok = launch_ring_n<1, 4, 1>(a, out_kind, nsc, grid, lds, nslot, s);
+  else if (rc == 2 && rp == 4 && wp == 1) ok = launch_ring_n<2, 4, 1>(a, out_kind, nsc, grid, lds, nslot, s);
+  else if (rc == 2 && rp == 2 && wp == 2) ok = launch_ring_n<2, 2, 2>(a, out_kind, nsc, grid, lds, nslot, s);
+  else if (rc == 1 && rp == 4 && wp == 2) ok = launch_ring_n<1, 4, 2>(a, out_kind, nsc, grid, lds, nslot, s);
+  else if (rc == 1 && rp == 2 && wp == 4) ok = launch_ring_n<1, 2, 4>(a, out_kind, nsc, grid, lds, nslot, s);
+  else if (rc == 4 && rp == 1 && wp == 4) ok = launch_ring_n<4, 1, 4>(a, out_kind, nsc, grid, lds, nslot, s);
+  else ok = launch_ring_n<4, 2, 4>(a, out_kind, nsc, grid, lds, nslot, s);
+  FCE_CHECK(ok, "conv 1x1 ring: no instantiation for this K depth");
+  return launch_status("conv1x1_ring_kernel");
+}
+
+static int launch_lds1(const ConvArgs& a0, int out_kind, int rc, int rp, int wp, hipStream_t s) {
+  FCE_CHECK(lds1_cfg_ok(rc, rp, wp), "conv 1x1 LDS tile: bad configuration");
+  ConvArgs a = a0;
+  const int cotiles = (a.cout + 15) / 16, cb = (4 / wp) * rc, tpb = wp * rp * 16;
+  a.gx = (a.P + tpb - 1) / tpb;
+  a.gy = (cotiles + cb - 1) / cb;
+  FCE_CHECK(int64_t(a.gx) * a.gy < (int64_t(1) << 31), "conv 1x1 LDS tile: grid too large");
+  const int nsc = lds1_nsc(a.nsteps, rc);
+  const size_t lds = std::max(lds1_bytes(rp, wp, nsc), a.stg ? lds1_out_bytes(rc, rp, wp) : size_t(0));
+  const dim3 grid(unsigned(a.gx * a.gy));
+  if (rc == 1 && rp == 4 && wp == 1) launch_lds1_n<1, 4, 1>(a, out_kind, nsc, grid, lds, s);
+  else if (rc == 2 && rp == 4 && wp == 1) launch_lds1_n<2, 4, 1>(a, out_kind, nsc, grid, lds, s);
+  else if (rc == 2 && rp == 2 && wp == 2) launch_lds1_n<2, 2, 2>(a, out_kind, nsc, grid, lds, s);
+  else if (rc == 1 && rp == 4 && wp == 2) launch_lds1_n<1, 4, 2>(a, out_kind, nsc, grid, lds, s);
+  else if (rc == 1 && rp == 2 && wp == 4) launch_lds1_n<1, 2, 4>(a, out_kind, nsc, grid, lds, s);
+  else if (rc == 4 && rp == 1 && wp == 4) launch_lds1_n<4, 1, 4>(a, out_kind, nsc, grid, lds, s);
+  else launch_lds1_n<4, 2, 4>(a, out_kind, nsc, grid, lds, s);
+  return launch_status("conv1x1_lds_kernel");
+}
+
 // ============================================================================ 3x3, LDS halo tiles
 // For cin % 32 == 0.  A block (4 waves) owns a 2-D output tile of TW = 16 columns x TH = 4*RP rows
 // of one image and RC*16 couts; wave w owns rows [w*RP, w*RP+RP) (one 16-pixel B fragment per row).
@@ -635,17 +1033,17 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
         if (a.vec_ok && co0 + 3 < a.cout) {
           const h4 rv = *reinterpret_cast<const h4*>(ro);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
         } else {
           for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] += (float)ro[j];
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
         }
       }
       if (a.vec_ok && co0 + 3 < a.cout) {
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
       } else {
         for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) yo[j] = (_Float16)v[j];
+          if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
       }
     }
   }
@@ -756,17 +1154,17 @@ __global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
         if (a.vec_ok && co0 + 3 < a.cout) {
           const h4 rv = *reinterpret_cast<const h4*>(ro);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += (float)rv[j];
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
         } else {
           for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] += (float)ro[j];
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
         }
       }
       if (a.vec_ok && co0 + 3 < a.cout) {
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
       } else {
         for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) yo[j] = (_Float16)v[j];
+          if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
       }
     }
   }
@@ -846,14 +1244,14 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[p][j] += (float)v[p * S + kx][j] * wk[ky * 3 + kx][j];
+        for (int j = 0; j < 8; ++j) acc[p][j] = __builtin_fmaf((float)v[p * S + kx][j], wk[ky * 3 + kx][j], acc[p][j]);
   }
 #pragma unroll
   for (int p = 0; p < PX; ++p) {
     if (ox0 + p >= a.Wo) break;
     h8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[p][j]) : acc[p][j]);
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(a.act ? silu(acc[p][j]) : acc[p][j]);
     *reinterpret_cast<h8*>(a.y + (int64_t(row) * a.Wo + ox0 + p) * a.ycs + c0) = o;
   }
 }
@@ -906,12 +1304,12 @@ __global__ __launch_bounds__(256) void dwconv_rows_kernel(DwArgs a, int CS) {
         const h8 v = rows[ky * RW + ix * (CS >> 3) + g];
         const float* wt = wl + (ky * 3 + kx) * CS + 8 * g;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j] * wt[j];
+        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fmaf((float)v[j], wt[j], acc[j]);
       }
     }
     h8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(a.act ? silu(acc[j]) : acc[j]);
     *reinterpret_cast<h8*>(yr + int64_t(ox) * a.ycs + 8 * g) = o;
   }
 }
@@ -963,17 +1361,19 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
         if (ix < 0 || ix >= a.W) continue;
         const h8 v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix) * a.xcs);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j] * wk[ky * 3 + kx][j];
+        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fmaf((float)v[j], wk[ky * 3 + kx][j], acc[j]);
       }
     }
     h8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(a.act ? silu(acc[j]) : acc[j]);
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(a.act ? silu(acc[j]) : acc[j]);
     *reinterpret_cast<h8*>(yr + int64_t(ox) * a.ycs) = o;
   }
 }
 
-// Variants (bitwise-identical results; the executor autotunes `variant` per layer, -1 = default):
+// Variants (bitwise-identical results; the executor autotunes `variant` per layer, -1 = default).  All
+// three accumulate with explicit fmaf in (ky, kx) order and pin the result before the fp16 conversion,
+// so hipcc cannot contract them differently.
 //   0 pixel-quad (dwconv_kernel<S,4>)   1 row-staged LDS (dwconv_rows_kernel)   2 lane-contiguous
 int dwconv_variants(int c, int w, int* out, int cap) {
   int n = 0;
@@ -1453,6 +1853,24 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int rp : {1, 2})
         if (n < cap && stream_ok(stream_nsm(d.cin / 32), rc, rp)) out[n++] = 0x300 | rc | (rp << 4);
     }
+  if (d.k == 1 && d.stride == 1)  // LDS-staged 1x1: 0x400 | rc | rp << 4 | log2(wp) << 12
+    for (int wl = 0; wl < 3; ++wl)
+      for (int rc : {1, 2, 4})
+        for (int rp : {1, 2, 4}) {
+          const int wp = 1 << wl, cb = (4 / wp) * rc;
+          if (!lds1_cfg_ok(rc, rp, wp)) continue;
+          if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
+          if (n < cap) out[n++] = 0x400 | rc | (rp << 4) | (wl << 12);
+        }
+  if (d.k == 1 && d.stride == 1)  // persistent LDS ring 1x1: 0x500 | rc | rp << 4 | log2(wp) << 12
+    for (int wl = 0; wl < 3; ++wl)
+      for (int rc : {1, 2, 4})
+        for (int rp : {1, 2, 4}) {
+          const int wp = 1 << wl, cb = (4 / wp) * rc;
+          if (!ring_ok((d.cin / 8 + 3) / 4, rc, rp, wp)) continue;
+          if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
+          if (n < cap) out[n++] = 0x500 | rc | (rp << 4) | (wl << 12);
+        }
   if (d.k == 3 && d.cin % 32 != 0 && d.cin <= 64 && d.up == 0 && !det_box)  // small-cin LDS tile: 0x200 | ..
     for (int rc : {1, 2, 4}) {
       if (rc > 1 && (rc >> 1) >= cotiles) continue;
@@ -1702,6 +2120,12 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.cmagic = g.cpt > 1 ? unsigned(0xFFFFFFFFull / unsigned(g.cpt) + 1ull) : 0u;
   FCE_CHECK(g.nalloc >= ((g.nsteps + 7) & ~7) + 8 && g.nchunk + 64 < 65536, "conv: K too large for the chunk cursor");
   a.vec_ok = (y.cstride % 4 == 0 && y.coff % 4 == 0 && (!res || (res->cstride % 4 == 0 && res->coff % 4 == 0))) ? 1 : 0;
+  static const bool no_stg = [] {
+    const char* e = getenv("FCE_NO_STG");
+    return e && atoi(e) != 0;
+  }();
+  a.stg = !no_stg && (out_kind == OUT_F16 || out_kind == OUT_WSTORE) && y.dtype == FCE_F16 && d.cout % 8 == 0 &&
+          y.cstride % 8 == 0 && y.coff % 8 == 0 && a.vec_ok;
   if (out_kind == OUT_WSTORE || out_kind == OUT_ACCUM) FCE_CHECK(d.fusion_w && d.fusion_n > d.fusion_i, "conv: fusion weights");
   a.pred = det ? det->pred : nullptr;
   a.det_A = det ? det->anchors : 0;
@@ -1712,6 +2136,22 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_stride = det ? det->stride : 0.f;
   const bool fast = d.cin % 32 == 0;
   int rc, rp;
+  if (tile >= 0 && (tile & 0xF00) == 0x500) {  // persistent LDS ring 1x1 kernel
+    rc = tile & 15;
+    rp = (tile >> 4) & 15;
+    const int wp = 1 << ((tile >> 12) & 3);
+    FCE_CHECK(d.k == 1 && d.stride == 1 && ring_ok(g.nsteps, rc, rp, wp), "conv: bad 1x1 ring hint");
+    if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && wp == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
+    return launch_ring(a, out_kind, rc, rp, wp, s);
+  }
+  if (tile >= 0 && (tile & 0xF00) == 0x400) {  // LDS-staged 1x1 kernel
+    rc = tile & 15;
+    rp = (tile >> 4) & 15;
+    const int wp = 1 << ((tile >> 12) & 3);
+    FCE_CHECK(d.k == 1 && d.stride == 1 && lds1_cfg_ok(rc, rp, wp), "conv: bad LDS 1x1 hint");
+    if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && wp == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
+    return launch_lds1(a, out_kind, rc, rp, wp, s);
+  }
   if (tile >= 0x300) {  // streaming 1x1 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;

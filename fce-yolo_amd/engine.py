@@ -89,6 +89,19 @@ class Engine:
     def num_ops(self) -> int:
         return N.lib().fce_net_num_ops(self.be.net)
 
+    def variants(self, i: int) -> list[int]:
+        """Candidate kernel variants of conv op i (empty for other ops)."""
+        codes = (C.c_int * 64)()
+        nv = N.lib().fce_net_op_variants(self.be.net, i, C.cast(codes, C.c_void_p), 64)
+        return list(codes[:nv])
+
+    def variant(self, i: int) -> int:
+        return N.lib().fce_net_op_variant(self.be.net, i)
+
+    def set_variant(self, i: int, code: int) -> None:
+        """Pin conv op i to one of its candidates (-1 = heuristic); every candidate is bitwise equal."""
+        N.call("fce_net_set_op_variant", self.be.net, i, code)
+
     def arena_bytes(self) -> int:
         return N.lib().fce_net_arena_bytes(self.be.net)
 

@@ -236,6 +236,11 @@ int fce_net_op_info(const fce_net* net, int i, char* name, int name_cap, double*
 int fce_net_buffer(const fce_net* net, int id, fce_tensor* out);
 /* kernel variant code the plan-time autotune chose for op i (-1 = heuristic / not tunable) */
 int fce_net_op_variant(const fce_net* net, int i);
+/* Candidate kernel variants of conv op i (as fce_conv_variants, for the planned shapes); 0 for other ops. */
+int fce_net_op_variants(const fce_net* net, int i, int* codes, int cap);
+/* Pin conv op i to a candidate variant (-1 = heuristic), e.g. to replay a tuning recorded elsewhere or to
+ * check variants against each other; results are bitwise the same for every candidate. */
+int fce_net_set_op_variant(fce_net* net, int i, int code);
 /* k-th autotune measurement of the last plan: op index, variant code, ms per run; returns 0 past the end */
 int fce_net_tune_record(const fce_net* net, int k, int* op, int* code, float* ms);
 

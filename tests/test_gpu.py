@@ -262,8 +262,59 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (48, 64, 3, 1, 21, 35, False), (24, 40, 3, 2, 19, 31, False), (64, 64, 3, 1, 40, 40, True),
     (32, 16, 1, 1, 30, 30, False), (96, 80, 3, 2, 23, 29, False), (128, 64, 3, 1, 20, 20, False),
     (128, 64, 1, 1, 25, 27, True), (256, 40, 1, 1, 16, 24, False), (96, 48, 1, 1, 41, 17, False),
-    (64, 128, 1, 1, 30, 40, False),
+    (64, 128, 1, 1, 30, 40, False), (384, 64, 1, 1, 13, 17, True), (264, 48, 1, 1, 9, 11, False),
+    (576, 256, 1, 1, 5, 7, False), (32, 32, 1, 1, 256, 256, False), (64, 48, 1, 1, 200, 200, True),
+    (192, 128, 1, 1, 128, 160, False),
 ]
+
+
+@pytest.mark.parametrize("cin,cout,up,xpad,ypad,epi", [
+    (64, 32, 1, 16, 8, N.EPI_STORE), (96, 128, 1, 0, 32, N.EPI_STORE), (48, 24, 0, 24, 16, N.EPI_STORE),
+    (256, 64, 2, 8, 0, N.EPI_STORE), (256, 64, 1, 0, 64, N.EPI_WSTORE), (128, 64, 0, 0, 0, N.EPI_WSTORE),
+    (256, 64, 1, 0, 64, N.EPI_ACCUM), (64, 128, 0, 32, 0, N.EPI_ACCUM)])
+def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, device):
+    """1x1 variants on channel-slice views (input and output inside wider NHWC buffers), with fused
+    nearest upsampling of the input and the BiFPN weighted-store / accumulate epilogues: bitwise equal
+    across variants, fp64-reference parity, and the output buffer's other channels untouched."""
+    H, W = 20, 20
+    g = torch.Generator().manual_seed(cin + 7 * cout + up + 100 * epi)
+    w = torch.randn(cout, cin, 1, 1, generator=g) * (1.0 / cin ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(2, cin, H, W, generator=g).half()
+    fw = torch.tensor([0.7, -0.2, 1.3])
+    fwd = fw.to(device)
+    desc = N.ConvDesc(cin, cout, 1, 1, 1, N.ACT_SILU, up, epi, fwd.data_ptr() if epi else None, 3 if epi else 0,
+                      2 if epi else 0)
+    wp = M.pack_conv(desc, w, device)
+    bd = b.float().to(device)
+    xbuf = torch.randn(2, H, W, cin + xpad, generator=g).half().to(device)
+    xbuf[..., xpad:] = x.to(device).permute(0, 2, 3, 1)
+    Ho, Wo = H << up, W << up
+    xu = x.double().repeat_interleave(1 << up, 2).repeat_interleave(1 << up, 3)
+    ref = torch.nn.functional.silu(torch.nn.functional.conv2d(xu, w.double(), b.double()))
+    y0 = torch.randn(2, Ho, Wo, cout, generator=g).half()
+    if epi:
+        r = fw.clamp_min(0).double()
+        alpha = r[2] / (r.sum() + 1e-4)
+        ref = alpha * ref + (y0.permute(0, 3, 1, 2).double() if epi == N.EPI_ACCUM else 0)
+    xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, 2, cin, H, W, cin + xpad, xpad)
+    codes = (C.c_int * 64)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 64)
+    assert any((codes[i] & 0xF00) == 0x400 for i in range(nv))
+    outs = {}
+    for code in [-1] + list(codes[:nv]):
+        y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
+        y[..., ypad:] = y0.to(device)
+        yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout + ypad, ypad)
+        N.call("fce_conv2d_variant", C.byref(desc), C.byref(xt), wp.data_ptr(), bd.data_ptr(), None, C.byref(yt),
+               code, None)
+        yc = y.cpu()
+        assert torch.isnan(yc[..., :ypad]).all(), hex(code)
+        outs[code] = yc[..., ypad:].permute(0, 3, 1, 2)
+    base = outs[-1]
+    for code, y in outs.items():
+        assert torch.equal(y, base), (hex(code), (y.float() - base.float()).abs().max().item())
+    assert _rel(base, ref) <= 4e-3
 
 
 @pytest.mark.parametrize("case", CONV_VARIANT_CASES)
@@ -302,3 +353,27 @@ def test_conv_every_variant_bitwise_and_parity(case, device):
     for code, y in outs.items():
         assert torch.equal(y, base), hex(code)
     assert _rel(base, ref) <= 4e-3
+
+
+@pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11s-bifpn.yaml", 2, 256),
+                                             ("yolo11n-fce.yaml", 1, 640)])
+def test_every_op_variant_bitwise_in_model(cfg, batch, imgsz, device, monkeypatch):
+    """Each conv op of a planned model, pinned in turn to every candidate kernel variant, leaves the
+    whole forward bitwise unchanged (the model's own views, upsampling, BiFPN / Detect epilogues and
+    partial tiles; this is what keeps batch invariance under plan-time autotuning)."""
+    monkeypatch.setenv("FCE_AUTOTUNE", "0")
+    model = cases.seeded_model(cfg, 0).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(3)).half().to(device)
+    eng = Engine(model, batch, imgsz, device)
+    base = eng(x).clone()
+    bad, tried = [], 0
+    for i in range(eng.num_ops()):
+        codes = eng.variants(i)
+        for code in codes:
+            eng.set_variant(i, code)
+            tried += 1
+            if not torch.equal(eng(x), base):
+                bad.append((i, hex(code)))
+        if codes:
+            eng.set_variant(i, -1)
+    assert tried > 100 and not bad, bad
