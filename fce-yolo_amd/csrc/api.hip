@@ -711,9 +711,9 @@ static int autotune(fce_net* net) {
   fce_tensor none{};
   for (OpDesc& op : net->ops) {
     if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
-    int cand[48];
+    int cand[128];
     const int nc_ = conv_tile_candidates(op.conv, op.kind == OP_CONV_DETECT && op.part == 0,
-                                         net->W >> net->bufs[op.in].shift, cand, 48);
+                                         net->W >> net->bufs[op.in].shift, cand, 128);
     if (nc_ <= 1) continue;
     float best_ms = 1e30f;
     int best = -1;
@@ -938,8 +938,8 @@ int fce_net_set_op_variant(fce_net* net, int i, int code) {
   OpDesc& op = net->ops[i];
   FCE_CHECK((op.kind == OP_CONV && op.in >= 0) || op.kind == OP_CONV_DETECT, "fce_net_set_op_variant: not a conv op");
   if (code != -1) {
-    int cand[48];
-    const int nc = fce_net_op_variants(net, i, cand, 48);
+    int cand[128];
+    const int nc = fce_net_op_variants(net, i, cand, 128);
     FCE_CHECK(std::find(cand, cand + nc, code) != cand + nc, "fce_net_set_op_variant: not a candidate of this op");
   }
   op.tile = code;

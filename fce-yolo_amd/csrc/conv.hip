@@ -947,13 +947,36 @@ static int launch_lds1(const ConvArgs& a0, int out_kind, int rc, int rp, int wp,
 // re-fetching the pixels from L2 as the implicit-GEMM kernel does.  A fragments: the same packed
 // layout (K-step = chunk * 9 + tap).  Per output element the K order (chunk-major, tap, channel)
 // is the implicit-GEMM kernel's, so both kernels give bitwise-identical results.
-template <int S, int RC, int RP>
+// LDS image of a staged tile: pixel (r, c) at position u = r * CI + tile_col(c), its four 16-byte
+// channel pieces q at slot q ^ ((u >> 1) & 3).  For stride 2 the even input columns come first, then
+// the odd ones, so the 16 lanes of a B fragment (output columns col * 2 + kx) read 16 consecutive
+// positions for every tap; with the XOR every ds_read_b128 lane group then meets 16 distinct 16-byte
+// slots of the bank row (was 2-way at stride 1 and 4-way at stride 2).
+template <int S, int CI>
+__device__ __forceinline__ int tile_col(int c) {
+  if (S == 1) return c;
+  return (c & 1) ? (CI + 1) / 2 + (c >> 1) : (c >> 1);
+}
+
+// Tile-kernel geometry (template): CW waves split the block's cout tiles (CW*RC of them), the other
+// 4/CW split its rows (RP rows each, TH = (4/CW)*RP); KP 32-channel chunks are staged per barrier
+// (KP = 2: 128 bytes per pixel, full-line loads, half the barriers).  Slot swizzle of the 4*KP pieces
+// of position u: q ^ ((u >> 1) & 3) for KP = 1, q ^ (u & 6) for KP = 2 (both conflict-free for the
+// B-fragment reads at any alignment; checked exhaustively over the ds_read_b128 lane groups).
+template <int KP>
+__device__ __forceinline__ int tile_slot(int u, int q) {
+  return KP == 1 ? (q ^ ((u >> 1) & 3)) : (q ^ (u & 6));
+}
+
+template <int S, int RC, int RP, int CW, int KP>
 __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
-  constexpr int TW = 16, TH = 4 * RP;
+  constexpr int TW = 16, RW = 4 / CW, TH = RW * RP;
   constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;  // staged input rows / cols
-  __shared__ __attribute__((aligned(16))) h8 tile[RI * CI * 4];  // [row][col][4 x 8 channels]
+  constexpr int NQ = 4 * KP;                                    // 16-byte pieces per staged pixel
+  __shared__ __attribute__((aligned(16))) h8 tile[RI * CI * NQ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / RW, wr = wave - wc * RW;
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   int t = blockIdx.x;
   const int tx = t % tiles_x;
@@ -961,7 +984,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
   const int ty = t % tiles_y;
   const int n = t / tiles_y;
   const int ox0 = tx * TW, oy0 = ty * TH;
-  const int cot0 = blockIdx.y * RC;
+  const int cot0 = (blockIdx.y * CW + wc) * RC;
   const int cotiles = (a.cout + 15) >> 4;
   const int spt = a.cin >> 5;  // 32-channel chunks = K-steps per tap
   const h8* wfrag[RC];
@@ -977,33 +1000,40 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
     for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
   const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-  for (int cc = 0; cc < spt; ++cc) {
-    __syncthreads();  // previous chunk's reads done
-    for (int e = threadIdx.x; e < RI * CI * 4; e += 256) {
-      const int pc = e >> 2, q = e & 3;
+  for (int c0 = 0; c0 < spt; c0 += KP) {
+    __syncthreads();  // previous stage's reads done
+    for (int e = threadIdx.x; e < RI * CI * NQ; e += 256) {
+      const int pc = e / NQ, q = e - pc * NQ;
       const int r = pc / CI, c = pc - r * CI;
       const int iy = iy0 + r, ix = ix0 + c;
       h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws)
-        v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + cc * 32 + q * 8);
-      tile[e] = v;
+      if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws && (KP == 1 || c0 + (q >> 2) < spt))
+        v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + c0 * 32 + q * 8);
+      const int u = r * CI + tile_col<S, CI>(c);
+      tile[u * NQ + tile_slot<KP>(u, q)] = v;
     }
     __syncthreads();
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - ky * 3;
-      h8 af[RC], bf[RP];
+    for (int k = 0; k < KP; ++k) {
+      if (KP > 1 && c0 + k >= spt) break;
 #pragma unroll
-      for (int r = 0; r < RC; ++r) af[r] = wfrag[r][(cc * 9 + tap) * 64];
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        h8 af[RC], bf[RP];
 #pragma unroll
-      for (int p = 0; p < RP; ++p) {
-        const int ry = (wave * RP + p) * S + ky, cx = col * S + kx;
-        bf[p] = tile[(ry * CI + cx) * 4 + grp];
+        for (int r = 0; r < RC; ++r) af[r] = wfrag[r][((c0 + k) * 9 + tap) * 64];
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int ry = (wr * RP + p) * S + ky;
+          const int u = ry * CI + tile_col<S, CI>(col * S + kx);
+          bf[p] = tile[u * NQ + tile_slot<KP>(u, k * 4 + grp)];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
       }
-#pragma unroll
-      for (int r = 0; r < RC; ++r)
-#pragma unroll
-        for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
     }
   }
   // epilogue: bias, SiLU, optional residual, fp16 NHWC store
@@ -1018,7 +1048,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
     for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
-      const int oy = oy0 + wave * RP + p;
+      const int oy = oy0 + wr * RP + p;
       if (oy >= a.Ho) continue;
       const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
       float v[4];
@@ -1828,6 +1858,15 @@ static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, 
     launch_dense_rp<KS, 4>(a, out_kind, fast, rc, s);
 }
 
+// Tile-kernel configurations, coded 0x100 | rc | rp << 4 | log2(cw) << 12 | (kp - 1) << 14
+static constexpr size_t tile3_lds(int s, int rp, int cw, int kp) {
+  return size_t(((4 / cw) * rp - 1) * s + 3) * (15 * s + 3) * 4 * kp * 16;
+}
+static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
+  return (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4) && (cw == 1 || cw == 2 || cw == 4) &&
+         (kp == 1 || kp == 2) && rc * rp <= 16 && tile3_lds(s, rp, cw, kp) <= 80 * 1024;
+}
+
 // Register tiles a dense conv may run with, encoded rc | rp << 4, or depthwise kernel variants,
 // encoded 100 + variant (the executor times them at plan time and keeps the fastest; neither
 // changes the per-output summation order, so results are bitwise the same for every choice).
@@ -1877,33 +1916,55 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int rp : {1, 2, 4})
         if (n < cap && small_tile_lds(d.stride, rp, d.cin) <= 64 * 1024) out[n++] = 0x200 | rc | (rp << 4);
     }
-  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel, coded 0x100 | rc | rp << 4
-    for (int rc : {1, 2, 4}) {
-      if (rc > 1 && (rc >> 1) >= cotiles) continue;
-      for (int rp : {1, 2, 4})
-        if (n < cap) out[n++] = 0x100 | rc | (rp << 4);
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel: 0x100 | rc | rp << 4 | cw, kp bits
+    for (int kp : {1, 2}) {
+      if (kp == 2 && d.cin % 64 != 0) continue;
+      for (int cwl = 0; cwl < 3; ++cwl)
+        for (int rc : {1, 2, 4}) {
+          const int cb = (1 << cwl) * rc;
+          if (cb > 1 && (cb >> 1) >= cotiles) continue;
+          for (int rp : {1, 2, 4})
+            if (n < cap && tile3_ok(d.stride, rc, rp, 1 << cwl, kp))
+              out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14);
+        }
     }
   return n;
 }
 
-template <int S, int RC>
-static void launch_tile3_rc(const ConvArgs& a, int rp, dim3 grid, hipStream_t s) {
-  if (rp == 1)
-    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 1>), grid, dim3(256), 0, s, a);
-  else if (rp == 2)
-    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 2>), grid, dim3(256), 0, s, a);
+template <int S, int RC, int RP, int CW, int KP>
+static void launch_tile3_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (tile3_lds(S, RP, CW, KP) <= 80 * 1024)
+    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, RP, CW, KP>), grid, dim3(256), 0, s, a);
+}
+
+template <int S, int RC, int RP>
+static void launch_tile3_w(const ConvArgs& a, int cw, int kp, dim3 grid, hipStream_t s) {
+  if (cw == 1)
+    kp == 1 ? launch_tile3_k<S, RC, RP, 1, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 1, 2>(a, grid, s);
+  else if (cw == 2)
+    kp == 1 ? launch_tile3_k<S, RC, RP, 2, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 2, 2>(a, grid, s);
   else
-    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, 4>), grid, dim3(256), 0, s, a);
+    kp == 1 ? launch_tile3_k<S, RC, RP, 4, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 4, 2>(a, grid, s);
+}
+
+template <int S, int RC>
+static void launch_tile3_rc(const ConvArgs& a, int rp, int cw, int kp, dim3 grid, hipStream_t s) {
+  if (rp == 1)
+    launch_tile3_w<S, RC, 1>(a, cw, kp, grid, s);
+  else if (rp == 2)
+    launch_tile3_w<S, RC, 2>(a, cw, kp, grid, s);
+  else
+    launch_tile3_w<S, RC, 4>(a, cw, kp, grid, s);
 }
 
 template <int S>
-static void launch_tile3_s(const ConvArgs& a, int rc, int rp, dim3 grid, hipStream_t s) {
+static void launch_tile3_s(const ConvArgs& a, int rc, int rp, int cw, int kp, dim3 grid, hipStream_t s) {
   if (rc == 1)
-    launch_tile3_rc<S, 1>(a, rp, grid, s);
+    launch_tile3_rc<S, 1>(a, rp, cw, kp, grid, s);
   else if (rc == 2)
-    launch_tile3_rc<S, 2>(a, rp, grid, s);
+    launch_tile3_rc<S, 2>(a, rp, cw, kp, grid, s);
   else
-    launch_tile3_rc<S, 4>(a, rp, grid, s);
+    launch_tile3_rc<S, 4>(a, rp, cw, kp, grid, s);
 }
 
 template <int S, int RC>
@@ -1940,15 +2001,16 @@ static int launch_small3(const ConvArgs& a, int rc, int rp, int stride, int n, h
   return launch_status("conv3x3_tile_small_kernel");
 }
 
-static int launch_tile3(const ConvArgs& a, int rc, int rp, int stride, int n, hipStream_t s) {
-  const int th = 4 * rp;
+static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, int stride, int n, hipStream_t s) {
+  FCE_CHECK(tile3_ok(stride, rc, rp, cw, kp), "conv 3x3 tile: bad configuration");
+  const int th = (4 / cw) * rp;
   const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
   FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
-  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + rc - 1) / rc));
+  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + cw * rc - 1) / (cw * rc)));
   if (stride == 1)
-    launch_tile3_s<1>(a, rc, rp, grid, s);
+    launch_tile3_s<1>(a, rc, rp, cw, kp, grid, s);
   else
-    launch_tile3_s<2>(a, rc, rp, grid, s);
+    launch_tile3_s<2>(a, rc, rp, cw, kp, grid, s);
   return launch_status("conv3x3_tile_kernel");
 }
 
@@ -2136,7 +2198,8 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_stride = det ? det->stride : 0.f;
   const bool fast = d.cin % 32 == 0;
   int rc, rp;
-  if (tile >= 0 && (tile & 0xF00) == 0x500) {  // persistent LDS ring 1x1 kernel
+  const int kind = tile >= 0 ? (tile >> 8) & 15 : -1;
+  if (kind == 5) {  // persistent LDS ring 1x1 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;
     const int wp = 1 << ((tile >> 12) & 3);
@@ -2144,7 +2207,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && wp == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
     return launch_ring(a, out_kind, rc, rp, wp, s);
   }
-  if (tile >= 0 && (tile & 0xF00) == 0x400) {  // LDS-staged 1x1 kernel
+  if (kind == 4) {  // LDS-staged 1x1 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;
     const int wp = 1 << ((tile >> 12) & 3);
@@ -2152,14 +2215,14 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && wp == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
     return launch_lds1(a, out_kind, rc, rp, wp, s);
   }
-  if (tile >= 0x300) {  // streaming 1x1 kernel
+  if (kind == 3) {  // streaming 1x1 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;
     FCE_CHECK(d.k == 1 && fast && (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2), "conv: bad stream hint");
     if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
     return launch_stream(a, out_kind, rc, rp, s);
   }
-  if (tile >= 0x200) {  // small-cin LDS tile 3x3 kernel
+  if (kind == 2) {  // small-cin LDS tile 3x3 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;
     FCE_CHECK(d.k == 3 && !fast && d.cin <= 64 && out_kind == OUT_F16 && d.up == 0 && (rc == 1 || rc == 2 || rc == 4) &&
@@ -2167,14 +2230,16 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
               "conv: bad small-cin LDS-tile hint");
     return launch_small3(a, rc, rp, d.stride, x.n, s);
   }
-  if (tile >= 0x100) {  // LDS halo-tile 3x3 kernel
+  if (kind == 1) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;
     rp = (tile >> 4) & 15;
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (rc == 1 || rc == 2 || rc == 4) &&
-                  (rp == 1 || rp == 2 || rp == 4),
+    const int cw = 1 << ((tile >> 12) & 3), kp = ((tile >> 14) & 1) + 1;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && tile3_ok(d.stride, rc, rp, cw, kp) &&
+                  (kp == 1 || d.cin % 64 == 0),
               "conv: bad LDS-tile hint");
-    return launch_tile3(a, rc, rp, d.stride, x.n, s);
+    return launch_tile3(a, rc, rp, cw, kp, d.stride, x.n, s);
   }
+  FCE_CHECK(kind <= 0, "conv: unknown kernel variant");
   if (tile >= 0) {
     rc = tile & 15;
     rp = tile >> 4;

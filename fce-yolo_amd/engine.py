@@ -91,8 +91,8 @@ class Engine:
 
     def variants(self, i: int) -> list[int]:
         """Candidate kernel variants of conv op i (empty for other ops)."""
-        codes = (C.c_int * 64)()
-        nv = N.lib().fce_net_op_variants(self.be.net, i, C.cast(codes, C.c_void_p), 64)
+        codes = (C.c_int * 128)()
+        nv = N.lib().fce_net_op_variants(self.be.net, i, C.cast(codes, C.c_void_p), 128)
         return list(codes[:nv])
 
     def variant(self, i: int) -> int:

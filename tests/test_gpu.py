@@ -298,8 +298,8 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
         alpha = r[2] / (r.sum() + 1e-4)
         ref = alpha * ref + (y0.permute(0, 3, 1, 2).double() if epi == N.EPI_ACCUM else 0)
     xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, 2, cin, H, W, cin + xpad, xpad)
-    codes = (C.c_int * 64)()
-    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 64)
+    codes = (C.c_int * 128)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     assert any((codes[i] & 0xF00) == 0x400 for i in range(nv))
     outs = {}
     for code in [-1] + list(codes[:nv]):
@@ -339,8 +339,8 @@ def test_conv_every_variant_bitwise_and_parity(case, device):
     ref = torch.nn.functional.silu(ref) + (r.double() if with_res else 0)
     xt = N.Tensor(xd.data_ptr(), N.F16, N.NHWC, 2, cin, H, W, cin, 0)
     rt = N.Tensor(res.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout, 0) if with_res else None
-    codes = (C.c_int * 64)()
-    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 64)
+    codes = (C.c_int * 128)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     assert nv >= 2
     outs = {}
     for code in [-1] + list(codes[:nv]):
