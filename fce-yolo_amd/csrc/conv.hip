@@ -14,6 +14,8 @@
 //   of 8 consecutive input channels of one pixel (coalesced along NHWC) per fragment; the
 //   weight fragments are pre-packed in exactly this lane order (1 KiB per fragment).
 //   D: lane l holds px = l&15, couts 4(l>>4)+0..3  -> 8-byte NHWC stores.
+#include <type_traits>
+
 #include "common.h"
 
 namespace fce {
@@ -763,7 +765,10 @@ __global__ __launch_bounds__(256) void conv1x1_ring_kernel(ConvArgs a, int nslot
 #pragma unroll
     for (int s = 0; s < NSC; ++s) af[s][r] = wf[s * 64];  // zero-padded past nsteps
   }
-  auto stage_load = [&](int tile, h8 (&v)[IT]) {
+  // (the upsampling branch is hoisted out of the unrolled loads: per-piece branches make hipcc wrap
+  // every load in its own exec branch)
+  auto stage_load_t = [&](auto up_tag, int tile, h8 (&v)[IT]) {
+    constexpr bool UP = decltype(up_tag)::value;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int e = threadIdx.x + 256 * i;
@@ -771,9 +776,15 @@ __global__ __launch_bounds__(256) void conv1x1_ring_kernel(ConvArgs a, int nslot
       const int p = rest / NPAIR, q = rest - p * NPAIR;
       const int pix = tile * TPB + p, c = q * 64 + j * 8;
       const bool ok = pix < a.P && c < a.cin;
-      v[i] = *(ok ? reinterpret_cast<const h8*>(a.x + conv1x1_src(a, pix) + c)
-                  : reinterpret_cast<const h8*>(g_zero_line));
+      const int64_t off = UP ? conv1x1_src(a, ok ? pix : 0) : int64_t(ok ? pix : 0) * a.xcs;
+      v[i] = *(ok ? reinterpret_cast<const h8*>(a.x + off + c) : reinterpret_cast<const h8*>(g_zero_line));
     }
+  };
+  auto stage_load = [&](int tile, h8 (&v)[IT]) {
+    if (a.up)
+      stage_load_t(std::true_type{}, tile, v);
+    else
+      stage_load_t(std::false_type{}, tile, v);
   };
   auto stage_store = [&](int buf, const h8 (&v)[IT]) {
 #pragma unroll
@@ -859,6 +870,33 @@ static void launch_lds1_n(const ConvArgs& a, int out_kind, int nsc, dim3 grid, s
     launch_lds1_o<RC, RP, WP, (RC == 4 ? 4 : 8)>(a, out_kind, grid, lds, s);
 }
 
+// Persistent launches size their grid from the kernel's real occupancy (registers and LDS), queried
+// once per instantiation: blocks beyond one resident wave would start only when a first-wave block
+// finishes its whole tile sequence.
+static int cus_per_xcd() {
+  static const int v = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) {
+      (void)hipGetLastError();
+      n = 256;
+    }
+    return std::max(1, n / 8);
+  }();
+  return v;
+}
+template <typename K>
+static int blocks_per_cu(K kernel, size_t lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return std::max(1, n);
+}
+static int ring_slots(int units, int gy, int occ) {
+  return std::max(1, std::min((units + 7) / 8, cus_per_xcd() * occ / std::max(1, gy)));
+}
+
 static int ring_nsc(int nsteps) { return nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 6 ? 6 : nsteps <= 8 ? 8 : 0; }
 static bool ring_ok(int nsteps, int rc, int rp, int wp) {
   const int nsc = ring_nsc(nsteps);
@@ -866,8 +904,14 @@ static bool ring_ok(int nsteps, int rc, int rp, int wp) {
 }
 
 template <int RC, int RP, int WP, int NSC>
-static void launch_ring_o(const ConvArgs& a, int out_kind, dim3 grid, size_t lds, int nslot, hipStream_t s) {
-#define RING_L(O) FCE_LAUNCH((conv1x1_ring_kernel<RC, RP, WP, NSC, O>), grid, dim3(256), lds, s, a, nslot)
+static void launch_ring_o(const ConvArgs& a, int out_kind, dim3, size_t lds, int, hipStream_t s) {
+#define RING_L(O)                                                                                  \
+  {                                                                                                \
+    static const int occ = blocks_per_cu(conv1x1_ring_kernel<RC, RP, WP, NSC, O>, lds);            \
+    const int nslot = ring_slots(a.gx, a.gy, occ);                                                 \
+    FCE_LAUNCH((conv1x1_ring_kernel<RC, RP, WP, NSC, O>), dim3(unsigned(8 * a.gy * nslot)), dim3(256), lds, s, a, \
+               nslot);                                                                             \
+  }
   switch (out_kind) {
     case OUT_F16: RING_L(OUT_F16); break;
     case OUT_F32: RING_L(OUT_F32); break;
@@ -902,10 +946,9 @@ static int launch_ring(const ConvArgs& a0, int out_kind, int rc, int rp, int wp,
   a.gy = (cotiles + cb - 1) / cb;
   const int nsc = ring_nsc(a.nsteps);
   const size_t lds = 2 * lds1_bytes(rp, wp, nsc);
-  const int occ = std::max(1, std::min(4, int((160 * 1024) / lds)));  // blocks per CU the LDS allows
-  const int nslot = std::max(1, std::min((a.gx + 7) / 8, 32 * occ / a.gy));
-  FCE_CHECK(int64_t(8) * a.gy * nslot < (int64_t(1) << 31), "conv 1x1 ring: grid too large");
-  const dim3 grid(unsigned(8 * a.gy * nslot));
+  FCE_CHECK(int64_t(8) * a.gy * cus_per_xcd() * 8 < (int64_t(1) << 31), "conv 1x1 ring: grid too large");
+  const int nslot = 0;  // per instantiation, from its occupancy (launch_ring_o)
+  const dim3 grid(1);
   bool ok;
   if (rc == 1 && rp == 4 && wp == 1) ok = launch_ring_n<1, 4, 1>(a, out_kind, nsc, grid, lds, nslot, s);
   else if (rc == 2 && rp == 4 && wp == 1) ok = launch_ring_n<2, 4, 1>(a, out_kind, nsc, grid, lds, nslot, s);
@@ -958,85 +1001,12 @@ __device__ __forceinline__ int tile_col(int c) {
   return (c & 1) ? (CI + 1) / 2 + (c >> 1) : (c >> 1);
 }
 
-// Tile-kernel geometry (template): CW waves split the block's cout tiles (CW*RC of them), the other
-// 4/CW split its rows (RP rows each, TH = (4/CW)*RP); KP 32-channel chunks are staged per barrier
-// (KP = 2: 128 bytes per pixel, full-line loads, half the barriers).  Slot swizzle of the 4*KP pieces
-// of position u: q ^ ((u >> 1) & 3) for KP = 1, q ^ (u & 6) for KP = 2 (both conflict-free for the
-// B-fragment reads at any alignment; checked exhaustively over the ds_read_b128 lane groups).
-template <int KP>
-__device__ __forceinline__ int tile_slot(int u, int q) {
-  return KP == 1 ? (q ^ ((u >> 1) & 3)) : (q ^ (u & 6));
-}
-
-template <int S, int RC, int RP, int CW, int KP>
-__global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
-  constexpr int TW = 16, RW = 4 / CW, TH = RW * RP;
-  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;  // staged input rows / cols
-  constexpr int NQ = 4 * KP;                                    // 16-byte pieces per staged pixel
-  __shared__ __attribute__((aligned(16))) h8 tile[RI * CI * NQ];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int col = lane & 15, grp = lane >> 4;
-  const int wc = wave / RW, wr = wave - wc * RW;
-  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
-  int t = blockIdx.x;
-  const int tx = t % tiles_x;
-  t /= tiles_x;
-  const int ty = t % tiles_y;
-  const int n = t / tiles_y;
-  const int ox0 = tx * TW, oy0 = ty * TH;
-  const int cot0 = (blockIdx.y * CW + wc) * RC;
+// Epilogue of the 3x3 tile kernels: acc[r][p] = cout tile cot0 + r x output row oy0 + p (16 columns
+// from ox0, lane col); bias, SiLU, optional residual, fp16 NHWC store.
+template <int RC, int RP>
+__device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP], int n, int oy0, int ox0, int cot0,
+                                            int col, int grp) {
   const int cotiles = (a.cout + 15) >> 4;
-  const int spt = a.cin >> 5;  // 32-channel chunks = K-steps per tap
-  const h8* wfrag[RC];
-#pragma unroll
-  for (int r = 0; r < RC; ++r) {
-    const int ct = min(cot0 + r, cotiles - 1);
-    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
-  }
-  f4 acc[RC][RP];
-#pragma unroll
-  for (int r = 0; r < RC; ++r)
-#pragma unroll
-    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
-  const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
-  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-  for (int c0 = 0; c0 < spt; c0 += KP) {
-    __syncthreads();  // previous stage's reads done
-    for (int e = threadIdx.x; e < RI * CI * NQ; e += 256) {
-      const int pc = e / NQ, q = e - pc * NQ;
-      const int r = pc / CI, c = pc - r * CI;
-      const int iy = iy0 + r, ix = ix0 + c;
-      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws && (KP == 1 || c0 + (q >> 2) < spt))
-        v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + c0 * 32 + q * 8);
-      const int u = r * CI + tile_col<S, CI>(c);
-      tile[u * NQ + tile_slot<KP>(u, q)] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      if (KP > 1 && c0 + k >= spt) break;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap - ky * 3;
-        h8 af[RC], bf[RP];
-#pragma unroll
-        for (int r = 0; r < RC; ++r) af[r] = wfrag[r][((c0 + k) * 9 + tap) * 64];
-#pragma unroll
-        for (int p = 0; p < RP; ++p) {
-          const int ry = (wr * RP + p) * S + ky;
-          const int u = ry * CI + tile_col<S, CI>(col * S + kx);
-          bf[p] = tile[u * NQ + tile_slot<KP>(u, k * 4 + grp)];
-        }
-#pragma unroll
-        for (int r = 0; r < RC; ++r)
-#pragma unroll
-          for (int p = 0; p < RP; ++p)
-            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
-      }
-    }
-  }
-  // epilogue: bias, SiLU, optional residual, fp16 NHWC store
   const int ox = ox0 + col;
   if (ox >= a.Wo) return;
 #pragma unroll
@@ -1048,7 +1018,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
     for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
-      const int oy = oy0 + wr * RP + p;
+      const int oy = oy0 + p;
       if (oy >= a.Ho) continue;
       const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
       float v[4];
@@ -1076,6 +1046,206 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
           if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
       }
     }
+  }
+}
+
+// Tile-kernel geometry (template): CW waves split the block's cout tiles (CW*RC of them), the other
+// 4/CW split its rows (RP rows each, TH = (4/CW)*RP); KP 32-channel chunks are staged per barrier
+// (KP = 2: 128 bytes per pixel, full-line loads, half the barriers).  Slot swizzle of the 4*KP pieces
+// of position u: q ^ ((u >> 1) & 3) for KP = 1, q ^ (u & 6) for KP = 2 (both conflict-free for the
+// B-fragment reads at any alignment; checked exhaustively over the ds_read_b128 lane groups).
+template <int KP>
+__device__ __forceinline__ int tile_slot(int u, int q) {
+  return KP == 1 ? (q ^ ((u >> 1) & 3)) : (q ^ (u & 6));
+}
+
+template <int S, int RC, int RP, int CW, int KP>
+__global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
+  constexpr int TW = 16, RW = 4 / CW, TH = RW * RP;
+  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;  // staged input rows / cols
+  constexpr int NQ = 4 * KP;                                    // 16-byte pieces per staged pixel
+  constexpr int NE0 = RI * CI * NQ, NL0 = (NE0 + 255) / 256;
+  // with the register prefetch (NL0 <= 8) the image is padded to NL0 * 256 pieces so that the last
+  // staging round stores unconditionally (see conv3x3_ring_kernel)
+  __shared__ __attribute__((aligned(16))) h8 tile[NL0 <= 8 ? NL0 * 256 : NE0];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / RW, wr = wave - wc * RW;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int n = t / tiles_y;
+  const int ox0 = tx * TW, oy0 = ty * TH;
+  const int cot0 = (blockIdx.y * CW + wc) * RC;
+  const int cotiles = (a.cout + 15) >> 4;
+  const int spt = a.cin >> 5;  // 32-channel chunks = K-steps per tap
+  const h8* wfrag[RC];
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int ct = min(cot0 + r, cotiles - 1);
+    wfrag[r] = reinterpret_cast<const h8*>(a.w) + (size_t(ct) * a.nalloc) * 64 + lane;
+  }
+  f4 acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  // Staging: NL pieces per thread.  When they fit in registers (NL <= 8) the next stage's global
+  // loads are issued right after this stage's LDS image is complete, so they are in flight during
+  // this stage's MFMAs (register double buffer; one LDS image).
+  constexpr int NE = RI * CI * NQ, NL = (NE + 255) / 256;
+  constexpr bool PF = NL <= 8;
+  auto piece = [&](int e, int c0, int& u, int& slot) -> h8 {
+    const int pc = e / NQ, q = e - pc * NQ;
+    const int r = pc / CI, c = pc - r * CI;
+    const int iy = iy0 + r, ix = ix0 + c;
+    u = r * CI + tile_col<S, CI>(c);
+    slot = e < NE ? u * NQ + tile_slot<KP>(u, q) : e;
+    const bool ok = e < NE && iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws && (KP == 1 || c0 + (q >> 2) < spt);
+    return *(ok ? reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + c0 * 32 + q * 8)
+                : reinterpret_cast<const h8*>(g_zero_line));
+  };
+  h8 pv[PF ? NL : 1];
+  int ps[PF ? NL : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      int u;
+      pv[i] = piece(threadIdx.x + 256 * i, 0, u, ps[i]);
+    }
+  }
+  for (int c0 = 0; c0 < spt; c0 += KP) {
+    __syncthreads();  // previous stage's reads done
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) tile[ps[i]] = pv[i];
+    } else {
+      for (int e = threadIdx.x; e < NE; e += 256) {
+        int u, sl;
+        const h8 v = piece(e, c0, u, sl);
+        tile[sl] = v;
+      }
+    }
+    __syncthreads();
+    if constexpr (PF) {
+      if (c0 + KP < spt) {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          int u;
+          pv[i] = piece(threadIdx.x + 256 * i, c0 + KP, u, ps[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      if (KP > 1 && c0 + k >= spt) break;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+        h8 af[RC], bf[RP];
+#pragma unroll
+        for (int r = 0; r < RC; ++r) af[r] = wfrag[r][((c0 + k) * 9 + tap) * 64];
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int ry = (wr * RP + p) * S + ky;
+          const int u = ry * CI + tile_col<S, CI>(col * S + kx);
+          bf[p] = tile[u * NQ + tile_slot<KP>(u, k * 4 + grp)];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+      }
+    }
+  }
+  tile3_store<RC, RP>(a, acc, n, oy0 + wr * RP, ox0, cot0, col, grp);
+}
+
+// ============================================================================ 3x3, persistent, A in registers
+// For cin = 32 * NCH (NCH = 1, 2: the 32/64-channel 3x3 convs of the n/s scales, which the tile kernels
+// run far below the MFMA rate because every wave re-reads its weight fragments from L2 for each
+// 64-pixel tile).  Each wave owns ONE cout tile and keeps its 9 * NCH A fragments in registers for the
+// whole launch; the block (4 cout tiles) walks a sequence of TH = RP row x 16 column output tiles,
+// staging each tile's input (+ halo, all cin, 64 * NCH bytes per pixel, the swizzled image of the tile
+// kernels) in one of two LDS buffers while the previous tile computes (the next tile's global loads are
+// issued before this tile's MFMAs).  Block b: XCD b % 8, cout group, slot; tiles xcd + 8 (slot + k nslot).
+// K order (chunk, tap) is the implicit-GEMM kernel's: bitwise identical.
+template <int S, int RP, int NCH>
+__global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot) {
+  constexpr int TW = 16, TH = RP;
+  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
+  // BUF = NL * 256 >= NE: slots past NE absorb the dummy pieces of the last staging round, so every
+  // staging load and LDS store is unconditional (a guarded store lets hipcc sink the load under a
+  // branch and serialise the loads with vmcnt waits)
+  constexpr int NQ = 4 * NCH, NE = RI * CI * NQ, NL = (NE + 255) / 256, BUF = NL * 256;
+  constexpr int KP = NCH;  // slot swizzle of the tile kernels for 4 * NCH pieces per pixel
+  __shared__ __attribute__((aligned(16))) h8 tile[2 * BUF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int by = loc % a.gy, slot = loc / a.gy;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  const int ntiles = tiles_x * tiles_y * a.N;
+  int t = xcd + 8 * slot;
+  if (t >= ntiles) return;  // block-uniform
+  const int cot0 = by * 4 + wave;
+  const int cotiles = (a.cout + 15) >> 4;
+  h8 af[NCH * 9];
+  {
+    const h8* wf = reinterpret_cast<const h8*>(a.w) + (size_t(min(cot0, cotiles - 1)) * a.nalloc) * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < NCH * 9; ++k) af[k] = wf[k * 64];
+  }
+  auto stage_load = [&](int tt, h8 (&v)[NL], int (&sl)[NL]) {
+    const int tx = tt % tiles_x, r0 = tt / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
+    const int iy0 = ty * TH * S - 1, ix0 = tx * TW * S - 1;
+    const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int pc = e / NQ, q = e - pc * NQ;
+      const int r = pc / CI, c = pc - r * CI;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const int u = r * CI + tile_col<S, CI>(c);
+      sl[i] = e < NE ? u * NQ + tile_slot<KP>(u, q) : e;
+      const bool ok = e < NE && iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws;
+      v[i] = *(ok ? reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + q * 8)
+                  : reinterpret_cast<const h8*>(g_zero_line));
+    }
+  };
+  h8 v[NL];
+  int sl[NL];
+  stage_load(t, v, sl);
+  const int step = 8 * nslot;
+  for (int cur = 0; t < ntiles; cur ^= 1) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) tile[cur * BUF + sl[i]] = v[i];
+    __syncthreads();
+    const int tn = t + step;
+    const int tx = t % tiles_x, r0 = t / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
+    if (tn < ntiles) stage_load(tn, v, sl);
+    f4 acc[1][RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[0][p] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int u = (p * S + ky) * CI + tile_col<S, CI>(col * S + kx);
+          const h8 bf = tile[cur * BUF + u * NQ + tile_slot<KP>(u, k * 4 + grp)];
+          acc[0][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k * 9 + tap], bf, acc[0][p], 0, 0, 0);
+        }
+      }
+    tile3_store<1, RP>(a, acc, n, ty * TH, tx * TW, cot0, col, grp);
+    t = tn;
   }
 }
 
@@ -1916,6 +2086,9 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int rp : {1, 2, 4})
         if (n < cap && small_tile_lds(d.stride, rp, d.cin) <= 64 * 1024) out[n++] = 0x200 | rc | (rp << 4);
     }
+  if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.up == 0 && !det_box)  // persistent ring: 0x600 | rp << 4
+    for (int rp : {1, 2, 4})
+      if (n < cap) out[n++] = 0x600 | (rp << 4);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel: 0x100 | rc | rp << 4 | cw, kp bits
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
@@ -2012,6 +2185,40 @@ static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, int s
   else
     launch_tile3_s<2>(a, rc, rp, cw, kp, grid, s);
   return launch_status("conv3x3_tile_kernel");
+}
+
+template <int S, int RP, int NCH>
+static void launch_ring3_k(const ConvArgs& a, dim3, int ntiles, hipStream_t s) {
+  static const int occ = blocks_per_cu(conv3x3_ring_kernel<S, RP, NCH>, 0);
+  const int nslot = ring_slots(ntiles, a.gy, occ);
+  FCE_LAUNCH((conv3x3_ring_kernel<S, RP, NCH>), dim3(unsigned(8 * a.gy * nslot)), dim3(256), 0, s, a, nslot);
+}
+
+template <int S, int NCH>
+static void launch_ring3_s(const ConvArgs& a, int rp, dim3 grid, int nslot, hipStream_t s) {
+  if (rp == 1)
+    launch_ring3_k<S, 1, NCH>(a, grid, nslot, s);
+  else if (rp == 2)
+    launch_ring3_k<S, 2, NCH>(a, grid, nslot, s);
+  else
+    launch_ring3_k<S, 4, NCH>(a, grid, nslot, s);
+}
+
+
+static int launch_ring3(const ConvArgs& a0, int rp, int stride, hipStream_t s) {
+  FCE_CHECK((a0.cin == 32 || a0.cin == 64) && (rp == 1 || rp == 2 || rp == 4), "conv 3x3 ring: bad configuration");
+  ConvArgs a = a0;
+  const int nch = a.cin / 32;
+  const int64_t ntiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + rp - 1) / rp) * a.N;
+  FCE_CHECK(ntiles < (int64_t(1) << 30), "conv 3x3 ring: too many tiles");
+  a.gy = ((a.cout + 15) / 16 + 3) / 4;
+  const int nslot = int(ntiles);  // the leaf launcher turns the tile count into slots (occupancy)
+  const dim3 grid(1);
+  if (stride == 1)
+    nch == 1 ? launch_ring3_s<1, 1>(a, rp, grid, nslot, s) : launch_ring3_s<1, 2>(a, rp, grid, nslot, s);
+  else
+    nch == 1 ? launch_ring3_s<2, 1>(a, rp, grid, nslot, s) : launch_ring3_s<2, 2>(a, rp, grid, nslot, s);
+  return launch_status("conv3x3_ring_kernel");
 }
 
 int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
@@ -2229,6 +2436,11 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
                   (rp == 1 || rp == 2 || rp == 4),
               "conv: bad small-cin LDS-tile hint");
     return launch_small3(a, rc, rp, d.stride, x.n, s);
+  }
+  if (kind == 6) {  // persistent 3x3 ring, A in registers
+    rp = (tile >> 4) & 15;
+    FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && out_kind == OUT_F16 && d.up == 0, "conv: bad 3x3 ring hint");
+    return launch_ring3(a, rp, d.stride, s);
   }
   if (kind == 1) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;

@@ -1,4 +1,2 @@
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 500 python -u scripts/variant_check.py --batch 32 > gpurun_out/vc32.log 2>&1; echo rc=$?; tail -5 gpurun_out/vc32.log
-timeout -k 10 500 python -u scripts/variant_check.py --batch 1 > gpurun_out/vc1.log 2>&1; echo rc=$?; tail -5 gpurun_out/vc1.log
-timeout -k 10 500 python -u scripts/variant_check.py --batch 2 --imgsz 320 --model yolo11s-bifpn.yaml > gpurun_out/vcs.log 2>&1; echo rc=$?; tail -5 gpurun_out/vcs.log
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/pk3; export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --kernel-trace --output-format csv -d gpurun_out/pk3/a -o run -- python scripts/pmc_kernel.py > gpurun_out/pk3/a.log 2>&1; echo rc=$?; tail -3 gpurun_out/pk3/a.log

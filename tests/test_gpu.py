@@ -264,7 +264,8 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (128, 64, 1, 1, 25, 27, True), (256, 40, 1, 1, 16, 24, False), (96, 48, 1, 1, 41, 17, False),
     (64, 128, 1, 1, 30, 40, False), (384, 64, 1, 1, 13, 17, True), (264, 48, 1, 1, 9, 11, False),
     (576, 256, 1, 1, 5, 7, False), (32, 32, 1, 1, 256, 256, False), (64, 48, 1, 1, 200, 200, True),
-    (192, 128, 1, 1, 128, 160, False),
+    (192, 128, 1, 1, 128, 160, False), (32, 64, 3, 2, 90, 100, False), (64, 48, 3, 1, 130, 70, True),
+    (64, 80, 3, 2, 41, 37, False),
 ]
 
 
