@@ -1571,6 +1571,82 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
   }
 }
 
+// Column-run variant: thread = (output column ox, 8-channel group), consecutive lanes = consecutive
+// channel groups then columns, so every load / store instruction covers contiguous pixels (full
+// lines); each thread computes PY outputs down its column from (PY-1)*S+3 input rows, every loaded
+// row feeding all the outputs that use it.  Out-of-image taps are skipped (selects, no branches) and
+// each output accumulates its taps in (ky, kx) order with fmaf, like the other variants.
+template <int S, int PY>
+__global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
+  const int cg = a.C >> 3;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.Wo * cg) return;
+  const int ox = e / cg, g = e - ox * cg, c0 = g * 8;
+  const int bands = (a.Ho + PY - 1) / PY;
+  const int n = blockIdx.y / bands, oy0 = (blockIdx.y - n * bands) * PY;
+  float wk[9][8], acc[PY][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const f4 w0 = *reinterpret_cast<const f4*>(a.w + t * a.wcs + c0);
+    const f4 w1 = *reinterpret_cast<const f4*>(a.w + t * a.wcs + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wk[t][j] = w0[j];
+      wk[t][j + 4] = w1[j];
+    }
+  }
+  {
+    const f4 b0 = *reinterpret_cast<const f4*>(a.bias + c0), b1 = *reinterpret_cast<const f4*>(a.bias + c0 + 4);
+#pragma unroll
+    for (int p = 0; p < PY; ++p)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[p][j] = b0[j];
+        acc[p][j + 4] = b1[j];
+      }
+  }
+  const _Float16* xn = a.x + int64_t(n) * a.H * a.W * a.xcs + c0;
+  const int iy0 = oy0 * S - 1, ix0 = ox * S - 1;
+  bool cok[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) cok[kx] = ix0 + kx >= 0 && ix0 + kx < a.W;
+  constexpr int NR = (PY - 1) * S + 3;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int iy = iy0 + r;
+    const bool rin = iy >= 0 && iy < a.H;
+    h8 v[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const bool ok = rin && cok[kx];
+      v[kx] = *(ok ? reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix0 + kx) * a.xcs)
+                   : reinterpret_cast<const h8*>(g_zero_line));
+    }
+#pragma unroll
+    for (int p = 0; p < PY; ++p) {
+      const int ky = r - p * S;
+      if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const bool ok = rin && cok[kx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = __builtin_fmaf((float)v[kx][j], wk[ky * 3 + kx][j], acc[p][j]);
+          acc[p][j] = ok ? f : acc[p][j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < PY; ++p) {
+    if (oy0 + p >= a.Ho) break;
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(a.act ? silu(acc[p][j]) : acc[p][j]);
+    *reinterpret_cast<h8*>(a.y + ((int64_t(n) * a.Ho + oy0 + p) * a.Wo + ox) * a.ycs + c0) = o;
+  }
+}
+
 // Variants (bitwise-identical results; the executor autotunes `variant` per layer, -1 = default).  All
 // three accumulate with explicit fmaf in (ky, kx) order and pin the result before the fp16 conversion,
 // so hipcc cannot contract them differently.
@@ -1580,6 +1656,8 @@ int dwconv_variants(int c, int w, int* out, int cap) {
   if (n < cap) out[n++] = 0;
   if (n < cap && size_t(10) * 8 * sizeof(float) + size_t(3) * w * 8 * sizeof(_Float16) <= 64 * 1024) out[n++] = 1;
   if (n < cap && c / 8 <= 256) out[n++] = 2;
+  if (n < cap) out[n++] = 3;  // column runs of 2
+  if (n < cap) out[n++] = 4;  // column runs of 4
   return n;
 }
 
@@ -1619,6 +1697,21 @@ int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const fl
     else
       FCE_LAUNCH((dwconv_lanes_kernel<2>), dim3(y.n * Ho), dim3(threads), 0, s, a);
     return launch_status("dwconv_lanes_kernel");
+  }
+  if (variant == 3 || variant == 4) {
+    const int py = variant == 3 ? 2 : 4;
+    const int64_t rows = int64_t(y.n) * ((Ho + py - 1) / py);
+    FCE_CHECK(rows < 65536, "dwconv: too many row bands");
+    const dim3 g((Wo * (x.c / 8) + 255) / 256, unsigned(rows));
+    if (stride == 1 && py == 2)
+      FCE_LAUNCH((dwconv_cols_kernel<1, 2>), g, dim3(256), 0, s, a);
+    else if (stride == 1)
+      FCE_LAUNCH((dwconv_cols_kernel<1, 4>), g, dim3(256), 0, s, a);
+    else if (py == 2)
+      FCE_LAUNCH((dwconv_cols_kernel<2, 2>), g, dim3(256), 0, s, a);
+    else
+      FCE_LAUNCH((dwconv_cols_kernel<2, 4>), g, dim3(256), 0, s, a);
+    return launch_status("dwconv_cols_kernel");
   }
   constexpr int PX = 4;
   dim3 grid(((Wo + PX - 1) / PX * (x.c / 8) + 255) / 256, y.n * Ho);
