@@ -2134,6 +2134,14 @@ static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
 // encoded 100 + variant (the executor times them at plan time and keeps the fastest; neither
 // changes the per-output summation order, so results are bitwise the same for every choice).
 // Returns the count; 0 for the stem.
+static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (ring) variants
+  static const bool v = [] {
+    const char* e = getenv("FCE_NO_RING");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap) {
   if (is_stem(d)) return 0;
   if (is_dw(d)) {  // depthwise kernel variants, coded 100 + variant
@@ -2164,7 +2172,7 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
           if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
           if (n < cap) out[n++] = 0x400 | rc | (rp << 4) | (wl << 12);
         }
-  if (d.k == 1 && d.stride == 1)  // persistent LDS ring 1x1: 0x500 | rc | rp << 4 | log2(wp) << 12
+  if (d.k == 1 && d.stride == 1 && !no_ring())  // persistent LDS ring 1x1: 0x500 | rc | rp << 4 | log2(wp) << 12
     for (int wl = 0; wl < 3; ++wl)
       for (int rc : {1, 2, 4})
         for (int rp : {1, 2, 4}) {
@@ -2179,7 +2187,7 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int rp : {1, 2, 4})
         if (n < cap && small_tile_lds(d.stride, rp, d.cin) <= 64 * 1024) out[n++] = 0x200 | rc | (rp << 4);
     }
-  if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.up == 0 && !det_box)  // persistent ring: 0x600 | rp << 4
+  if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.up == 0 && !det_box && !no_ring())  // persistent: 0x600 | rp << 4
     for (int rp : {1, 2, 4})
       if (n < cap) out[n++] = 0x600 | (rp << 4);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel: 0x100 | rc | rp << 4 | cw, kp bits

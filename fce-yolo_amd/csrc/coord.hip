@@ -92,16 +92,19 @@ __global__ __launch_bounds__(256) void pool_cols_kernel(const _Float16* x, int x
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const _Float16* p = x + nhwc_off(n, 0, xx, H, W, xcs) + cg * 8;
   const int64_t rs = int64_t(W) * xcs;
+  // 8 rows in flight per step (the walk down a column is latency-bound otherwise); rows are still
+  // added in order, so the sum is the sequential one
   int y = 0;
-  for (; y + 1 < H; y += 2) {
-    const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
-    const h8 v1 = *reinterpret_cast<const h8*>(p + (y + 1) * rs);
+  for (; y + 7 < H; y += 8) {
+    h8 v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+    for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const h8*>(p + (y + k) * rs);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v1[j];
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)v[k][j];
   }
-  if (y < H) {
+  for (; y < H; ++y) {
     const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];

@@ -126,6 +126,122 @@ __global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16*
   }
 }
 
+// Chunked variant: K (swizzled [key][32], conflict-free fragment reads) and V^T for KC = 256 keys are
+// staged in LDS once per chunk with one barrier pair, and the four 64-key tiles of the chunk run back
+// to back from LDS (the per-tile kernel above has two barriers and a V transpose per 64 keys, and
+// reads K straight from L2 inside the dependency chain).  Same MFMA operands, the same online-softmax
+// order over 64-key tiles: bitwise-identical results.
+template <int KD, int HD>
+__global__ __launch_bounds__(256) void psa_attention_chunk_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
+                                                                  int ycs, float scale_log2) {
+  static_assert(KD == 32 && HD == 64, "C2PSA geometry");
+  constexpr int KT = 64, KC = 256, VTS = KC + 4;
+  __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VTS];
+  __shared__ __attribute__((aligned(16))) h8 kl[KC * 4];  // [key][4 x 8 dims], piece g at g ^ ((key >> 1) & 3)
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int q = blockIdx.x * 64 + wave * 16 + col;
+  const _Float16* base = qkv + int64_t(n) * N * qcs + hd * (2 * KD + HD);
+  h8 qf = h8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (q < N) qf = *reinterpret_cast<const h8*>(base + int64_t(q) * qcs + 8 * g);
+  float m = -INFINITY, l = 0.f;
+  f4 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < N; c0 += KC) {
+    __syncthreads();
+    // stage K rows and V^T of keys c0 .. c0 + KC - 1 (zeros past N)
+#pragma unroll
+    for (int i = 0; i < KC * 4 / 256; ++i) {
+      const int e = threadIdx.x + 256 * i, key = e >> 2, pc = e & 3;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (c0 + key < N) v = *reinterpret_cast<const h8*>(base + int64_t(c0 + key) * qcs + KD + 8 * pc);
+      kl[key * 4 + (pc ^ ((key >> 1) & 3))] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < KC * (HD / 8) / 256; ++i) {
+      const int e = threadIdx.x + 256 * i, key = e / (HD / 8), dc = (e % (HD / 8)) * 8;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (c0 + key < N) v = *reinterpret_cast<const h8*>(base + int64_t(c0 + key) * qcs + 2 * KD + dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(dc + j) * VTS + key] = v[j];
+    }
+    __syncthreads();
+    const int nt = min(KC, N - c0);
+    for (int k1 = 0; k1 < nt; k1 += KT) {
+      const int k0 = c0 + k1;
+      f4 s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int key = k1 + 16 * t + col;
+        const h8 kf = kl[key * 4 + (g ^ ((key >> 1) & 3))];
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = k0 + 16 * t + 4 * g + j;
+          const float v = key < N ? s[t][j] * scale_log2 : -INFINITY;
+          s[t][j] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16));
+      mt = fmaxf(mt, __shfl_xor(mt, 32));
+      const float mn = fmaxf(m, mt);
+      const float corr = exp2f(m - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f(s[t][j] - mn);
+          s[t][j] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      l = l * corr + rs;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[dt][j] *= corr;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        h8 pf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[j] = (_Float16)s[2 * u][j];
+          pf[j + 4] = (_Float16)s[2 * u + 1][j];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const _Float16* row = vt + (16 * dt + col) * VTS + k1 + 32 * u + 4 * g;
+          const h4 lo = *reinterpret_cast<const h4*>(row);
+          const h4 hi = *reinterpret_cast<const h4*>(row + 16);
+          const h8 vf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, acc[dt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (q >= N) return;
+  const float inv = 1.0f / l;
+  _Float16* yo = y + (int64_t(n) * N + q) * ycs + hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    _Float16* p = yo + 16 * dt + 4 * g;
+    const h4 pe = *reinterpret_cast<const h4*>(p);  // pe(v) written by the depthwise pass
+    h4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (_Float16)((float)pe[j] + acc[dt][j] * inv);
+    *reinterpret_cast<h4*>(p) = o;
+  }
+}
+
 int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, const float* pe_w, const float* pe_b,
                   const fce_tensor& y, hipStream_t s) {
   FCE_CHECK(qkv.layout == FCE_NHWC && y.layout == FCE_NHWC && qkv.dtype == FCE_F16 && y.dtype == FCE_F16,
@@ -151,10 +267,20 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
   }
   dim3 grid((N + 63) / 64, heads, qkv.n);
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)key_dim);
-  FCE_LAUNCH((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
-                     static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
-                     static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
-  return launch_status("psa_attention_mfma_kernel");
+  static const bool tiled = [] {  // diagnostics: FCE_PSA_TILED=1 runs the per-64-key-tile kernel
+    const char* e = getenv("FCE_PSA_TILED");
+    return e && atoi(e) != 0;
+  }();
+  if (tiled) {
+    FCE_LAUNCH((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
+               static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
+               static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
+    return launch_status("psa_attention_mfma_kernel");
+  }
+  FCE_LAUNCH((psa_attention_chunk_kernel<32, 64>), grid, dim3(256), 0, s,
+             static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
+             static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
+  return launch_status("psa_attention_chunk_kernel");
 }
 
 }  // namespace fce

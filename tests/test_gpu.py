@@ -378,3 +378,18 @@ def test_every_op_variant_bitwise_in_model(cfg, batch, imgsz, device, monkeypatc
         if codes:
             eng.set_variant(i, -1)
     assert tried > 100 and not bad, bad
+
+
+@pytest.mark.parametrize("hw", [(20, 23), (9, 7), (16, 16), (33, 20)])
+def test_c2psa_multi_chunk_vs_oracle(hw, device):
+    """C2PSA attention over more keys than one 256-key LDS chunk (and ragged 64-key tiles) vs the fp64
+    oracle restatement (block.py:1247-1304)."""
+    H, W = hw
+    fx = {"seed": np.array(62)}
+    mod = cases.build_op("c2psa", fx)
+    x = torch.randn(2, 256, H, W, generator=torch.Generator().manual_seed(H * 100 + W)).half()
+    ref = cases.oracle_op("c2psa", mod, [x.float()])
+    with torch.no_grad():
+        y = mod.to(device)(x.to(device))
+    assert torch.isfinite(y).all()
+    assert _rel(y.float(), ref) <= OP_TOL
