@@ -28,7 +28,12 @@ def family(name):
         if out == 5:
             return "conv1x1_detect_cls"
         return "conv3x3_mfma" if ks == 3 else "conv1x1_mfma"
-    for key, fam in (("conv3x3_tile", "conv3x3_mfma"), ("stem", "conv_stem"), ("psa_attention", "psa_attention"),
+    m = re.search(r"conv1x1_(?:lds|ring)_kernel<\d+, \d+, \d+, \d+, (\d)>", name) or \
+        re.search(r"conv1x1_stream_kernel<\d+, \d+, \d+, (\d)>", name)
+    if m:
+        out = int(m.group(1))
+        return "conv1x1_detect_box" if out == 4 else "conv1x1_detect_cls" if out == 5 else "conv1x1_mfma"
+    for key, fam in (("conv3x3_tile", "conv3x3_mfma"), ("conv3x3_ring", "conv3x3_mfma"), ("stem", "conv_stem"), ("psa_attention", "psa_attention"),
                      ("dwconv", "dwconv3x3"), ("maxpool", "maxpool_chain"), ("weighted_add", "bifpn_weighted_add"),
                      ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"),
                      ("coord_", "bicoordcrossatt"), ("gate_apply", "bicoordcrossatt"), ("nms", "nms"),
