@@ -1001,6 +1001,16 @@ __device__ __forceinline__ int tile_col(int c) {
   return (c & 1) ? (CI + 1) / 2 + (c >> 1) : (c >> 1);
 }
 
+// XCD-aware block order of the 3x3 tile kernels: the grid is 1-D (tiles x cout groups); block b runs on
+// XCD b % 8, so each XCD gets a contiguous range of logical blocks, cout groups innermost: the blocks that
+// stage the same input tile, and the neighbouring tiles that share its halo rows, hit one L2.
+__device__ __forceinline__ void tile_block(int gy, int& tile, int& cog) {
+  const int total = int(gridDim.x), b = int(blockIdx.x), per = total >> 3, body = per << 3;
+  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+  tile = L / gy;
+  cog = L - tile * gy;
+}
+
 // Epilogue of the 3x3 tile kernels: acc[r][p] = cout tile cot0 + r x output row oy0 + p (16 columns
 // from ox0, lane col); bias, SiLU, optional residual, fp16 NHWC store.
 template <int RC, int RP>
@@ -1072,13 +1082,14 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
   const int col = lane & 15, grp = lane >> 4;
   const int wc = wave / RW, wr = wave - wc * RW;
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
-  int t = blockIdx.x;
+  int t, cog;
+  tile_block(a.gy, t, cog);
   const int tx = t % tiles_x;
   t /= tiles_x;
   const int ty = t % tiles_y;
   const int n = t / tiles_y;
   const int ox0 = tx * TW, oy0 = ty * TH;
-  const int cot0 = (blockIdx.y * CW + wc) * RC;
+  const int cot0 = (cog * CW + wc) * RC;
   const int cotiles = (a.cout + 15) >> 4;
   const int spt = a.cin >> 5;  // 32-channel chunks = K-steps per tap
   const h8* wfrag[RC];
@@ -1266,13 +1277,14 @@ __global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
   const int col = lane & 15, grp = lane >> 4;
   const int cpt = a.cpt;
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
-  int t = blockIdx.x;
+  int t, cog;
+  tile_block(a.gy, t, cog);
   const int tx = t % tiles_x;
   t /= tiles_x;
   const int ty = t % tiles_y;
   const int n = t / tiles_y;
   const int ox0 = tx * TW, oy0 = ty * TH;
-  const int cot0 = blockIdx.y * RC;
+  const int cot0 = cog * RC;
   const int cotiles = (a.cout + 15) >> 4;
   const h8* wfrag[RC];
 #pragma unroll
@@ -2267,11 +2279,14 @@ static int launch_small3(const ConvArgs& a, int rc, int rp, int stride, int n, h
   FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 small tile: grid too large");
   const size_t lds = small_tile_lds(stride, rp, a.cin);
   FCE_CHECK(lds <= 64 * 1024, "conv 3x3 small tile: LDS tile too large");
-  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + rc - 1) / rc));
+  ConvArgs b = a;
+  b.gy = ((a.cout + 15) / 16 + rc - 1) / rc;
+  FCE_CHECK(tiles * b.gy < (int64_t(1) << 31), "conv 3x3 small tile: grid too large");
+  const dim3 grid(unsigned(tiles * b.gy));
   if (stride == 1)
-    launch_small3_s<1>(a, rc, rp, grid, lds, s);
+    launch_small3_s<1>(b, rc, rp, grid, lds, s);
   else
-    launch_small3_s<2>(a, rc, rp, grid, lds, s);
+    launch_small3_s<2>(b, rc, rp, grid, lds, s);
   return launch_status("conv3x3_tile_small_kernel");
 }
 
@@ -2280,11 +2295,14 @@ static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, int s
   const int th = (4 / cw) * rp;
   const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
   FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
-  const dim3 grid(unsigned(tiles), unsigned(((a.cout + 15) / 16 + cw * rc - 1) / (cw * rc)));
+  ConvArgs b = a;
+  b.gy = ((a.cout + 15) / 16 + cw * rc - 1) / (cw * rc);
+  FCE_CHECK(tiles * b.gy < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
+  const dim3 grid(unsigned(tiles * b.gy));
   if (stride == 1)
-    launch_tile3_s<1>(a, rc, rp, cw, kp, grid, s);
+    launch_tile3_s<1>(b, rc, rp, cw, kp, grid, s);
   else
-    launch_tile3_s<2>(a, rc, rp, cw, kp, grid, s);
+    launch_tile3_s<2>(b, rc, rp, cw, kp, grid, s);
   return launch_status("conv3x3_tile_kernel");
 }
 

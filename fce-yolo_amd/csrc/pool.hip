@@ -79,7 +79,14 @@ __device__ __forceinline__ h8 hmax8(h8 a, h8 b) { return __builtin_elementwise_m
 __global__ __launch_bounds__(256) void maxpool_chain_lds_kernel(MpArgs a) {
   extern __shared__ __attribute__((aligned(16))) h8 pl[];
   const int HW = a.H * a.W, cg = a.C >> 3;
-  const int n = blockIdx.x / cg, g = blockIdx.x - n * cg;
+  // XCD-aware order: block b runs on XCD b % 8; give each XCD a contiguous range of (image, group)
+  // pairs so an image's channel groups (16-byte pieces of the same 128-byte lines) share one L2
+  int L;
+  {
+    const int total = int(gridDim.x), b = int(blockIdx.x), per = total >> 3, body = per << 3;
+    L = b < body ? (b & 7) * per + (b >> 3) : b;
+  }
+  const int n = L / cg, g = L - n * cg;
   h8* xs = pl;
   h8* r1 = pl + HW;
   h8* r2 = pl + 2 * HW;
