@@ -1985,19 +1985,53 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float
   const int WP = a.W + 16;  // 16-byte zero pads left and right keep every staged chunk aligned
   const int CW = WP / 8;    // 16-byte chunks per staged row
   const T* x = static_cast<const T*>(a.x);
-  for (int e = threadIdx.x; e < a.C * IR * CW; e += 256) {
-    const int cr = e / CW, q = e - cr * CW;
-    const int ci = cr / IR, r = cr - ci * IR;
-    const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
-    h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W) {
-      const T* src = x + ((int64_t(n) * a.C + ci) * a.H + iy) * a.W + ix0;
-      RawRun<T, 8> run;
-      run.load(src);
+  const int ne = a.C * IR * CW;
+  if constexpr (std::is_same<T, _Float16>::value) {
+    // fp16 input: up to 12 staging chunks per thread issued back to back (address select onto a zero
+    // line, unconditional LDS stores), instead of one dependent load -> store round trip per chunk
+    constexpr int NLS = 12;
+    if (ne <= NLS * 256) {
+      h8 v[NLS];
+      int dst[NLS];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (_Float16)run.get(j);
+      for (int i = 0; i < NLS; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        const int cr = e / CW, q = e - cr * CW;
+        const int ci = cr / IR, r = cr - ci * IR;
+        const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
+        const bool ok = e < ne && iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W;
+        dst[i] = e < ne ? cr * WP + q * 8 : a.C * IR * WP;  // one 16-byte dummy slot past the image
+        v[i] = *(ok ? reinterpret_cast<const h8*>(x + ((int64_t(n) * a.C + ci) * a.H + iy) * a.W + ix0)
+                    : reinterpret_cast<const h8*>(g_zero_line));
+      }
+#pragma unroll
+      for (int i = 0; i < NLS; ++i) *reinterpret_cast<h8*>(ssm + dst[i]) = v[i];
+    } else {
+      for (int e = threadIdx.x; e < ne; e += 256) {
+        const int cr = e / CW, q = e - cr * CW;
+        const int ci = cr / IR, r = cr - ci * IR;
+        const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
+        const bool ok = iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W;
+        *reinterpret_cast<h8*>(ssm + cr * WP + q * 8) =
+            *(ok ? reinterpret_cast<const h8*>(x + ((int64_t(n) * a.C + ci) * a.H + iy) * a.W + ix0)
+                 : reinterpret_cast<const h8*>(g_zero_line));
+      }
     }
-    *reinterpret_cast<h8*>(ssm + cr * WP + q * 8) = v;
+  } else {
+    for (int e = threadIdx.x; e < ne; e += 256) {
+      const int cr = e / CW, q = e - cr * CW;
+      const int ci = cr / IR, r = cr - ci * IR;
+      const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
+      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W) {
+        const T* src = x + ((int64_t(n) * a.C + ci) * a.H + iy) * a.W + ix0;
+        RawRun<T, 8> run;
+        run.load(src);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)run.get(j);
+      }
+      *reinterpret_cast<h8*>(ssm + cr * WP + q * 8) = v;
+    }
   }
   // this lane's 8 k values: (ci, ky, kx) -> LDS offset relative to the pixel's window origin
   int koff[8];
@@ -2366,8 +2400,8 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     const int PX = coutT <= 32 ? 2 : 1;  // measured: PX 2 beats 4 (occupancy) and 1 (reuse) at cout 16
     const char* sv = getenv("FCE_STEM_VALU");  // diagnostics: the fp32 VALU stem instead of MFMA
     if (stem_mfma_ok(d) && d.stride == 2 && x.c == d.cin && d.cout % 16 == 0 && x.w % 8 == 0 &&
-        size_t(x.c) * 9 * (x.w + 16) * 2 <= 64 * 1024 && !(sv && atoi(sv))) {
-      const size_t lds = size_t(x.c) * 9 * (x.w + 16) * sizeof(_Float16);
+        size_t(x.c) * 9 * (x.w + 16) * 2 + 16 <= 64 * 1024 && !(sv && atoi(sv))) {
+      const size_t lds = size_t(x.c) * 9 * (x.w + 16) * sizeof(_Float16) + 16;  // + the dummy staging slot
       FCE_CHECK(lds <= 64 * 1024, "stem conv: input rows do not fit in LDS");
       const int64_t blocks2 = int64_t(x.n) * ((Ho + 3) / 4);
       FCE_CHECK(blocks2 < (int64_t(1) << 31), "stem conv: input too large");
