@@ -155,11 +155,36 @@ __global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP, in
   for (int k0 = 0; k0 < K; k0 += KC) {
     const int kc = min(KC, K - k0);
     __syncthreads();
-    for (int e = threadIdx.x; e < np * kc; e += 256) {
-      const int i = e / kc, c = e - i * kc;
-      ss[i * KC + c] = src[int64_t(i) * K + k0 + c];
+    // staging in rounds of 8 loads per thread issued back to back (a load -> LDS-store loop otherwise
+    // waits out one memory latency per element); loads use clamped indices and the stores of the
+    // out-of-range slots go to one dummy float past the weights, so neither is conditional
+    float* dummy = ws + KC * M;
+    const int n1 = np * kc, n2 = kc * M;
+    for (int e0 = 0; e0 < n1; e0 += 8 * 256) {
+      float v[8];
+      float* d[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + int(threadIdx.x) + 256 * u, ec = min(e, n1 - 1);
+        const int i = ec / kc, c = ec - i * kc;
+        v[u] = src[int64_t(i) * K + k0 + c];
+        d[u] = e < n1 ? ss + i * KC + c : dummy;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *d[u] = v[u];
     }
-    for (int e = threadIdx.x; e < kc * M; e += 256) ws[e] = jb.wt[int64_t(k0) * M + e];
+    for (int e0 = 0; e0 < n2; e0 += 8 * 256) {
+      float v[8];
+      float* d[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + int(threadIdx.x) + 256 * u;
+        v[u] = jb.wt[int64_t(k0) * M + min(e, n2 - 1)];
+        d[u] = e < n2 ? ws + e : dummy;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *d[u] = v[u];
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < OPT; ++i) {
@@ -287,10 +312,28 @@ __global__ __launch_bounds__(256) void coord_attend_groups_kernel(AttArgs a, int
   float* qs = ys + qper * mid;  // qper*mid: the block's queries
   const float* kg = jb.k + int64_t(n) * Lk * mid;
   const float* vg = jb.v + int64_t(n) * Lk * mid;
-  for (int e = threadIdx.x; e < Lk * mid; e += blockDim.x) {
-    const int j = e / mid, c = e - j * mid;
-    ks[j * ld + c] = kg[e];
-    vs[j * ld + c] = vg[e];
+  // K / V staging in rounds of 4 elements per thread (8 loads in flight; clamped loads, out-of-range
+  // stores to a dummy float past the queries, so nothing is conditional)
+  {
+    float* dummy = qs + qper * mid;
+    const int nkv = Lk * mid;
+    for (int e0 = 0; e0 < nkv; e0 += 4 * int(blockDim.x)) {
+      float kv[4], vv[4];
+      int dj[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + int(threadIdx.x) + u * int(blockDim.x), ec = min(e, nkv - 1);
+        const int j = ec / mid, c = ec - j * mid;
+        kv[u] = kg[ec];
+        vv[u] = vg[ec];
+        dj[u] = e < nkv ? j * ld + c : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        *(dj[u] >= 0 ? ks + dj[u] : dummy) = kv[u];
+        *(dj[u] >= 0 ? vs + dj[u] : dummy) = vv[u];
+      }
+    }
   }
   const float* qg0 = jb.q + (int64_t(n) * jb.Lq + q0) * mid;
   for (int e = threadIdx.x; e < nq * mid; e += blockDim.x) qs[e] = qg0[e];
@@ -400,7 +443,7 @@ static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
   FCE_CHECK(maxM <= 256 * 16, "coord projection: too many outputs");
   const int TP = std::max(1, std::min(16, 256 * 16 / maxM));                       // positions per block
   const int KC = std::max(1, std::min({maxK, 256, (8192 - TP * 64) / maxM}));      // <= 32 KiB of weights
-  const size_t shm = (size_t(TP) * KC + size_t(KC) * maxM) * sizeof(float);
+  const size_t shm = (size_t(TP) * KC + size_t(KC) * maxM + 1) * sizeof(float);  // + the staging dummy
   dim3 grid((maxL + TP - 1) / TP, nj, N);
   FCE_LAUNCH(coord_proj_kernel, grid, dim3(256), shm, s, pa, TP, KC);
   return launch_status("coord_proj_kernel");
@@ -430,7 +473,8 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
   const int tiles = (maxLq + a.QT - 1) / a.QT;
   const int per = std::max(1, std::min((tiles + 7) / 8, 32 / std::max(1, a.QT)));
   const int qper = per * a.QT;
-  size_t shm = (size_t(2) * maxLk * (groups ? (d.mid | 1) : d.mid) + size_t(groups ? 2 * qper : a.QT) * d.mid) *
+  size_t shm = (size_t(2) * maxLk * (groups ? (d.mid | 1) : d.mid) + size_t(groups ? 2 * qper : a.QT) * d.mid +
+                (groups ? 1 : 0)) *  // + the staging dummy of the grouped kernel
                sizeof(float);
   if (shm > kMaxLds) return fail(FCE_ERR_UNSUPPORTED, "coord attention: K/V do not fit in LDS");
   a.wlds = !groups && shm + size_t(d.mid) * d.oup * sizeof(float) <= kMaxLds;
