@@ -92,7 +92,20 @@ __global__ __launch_bounds__(256) void maxpool_chain_lds_kernel(MpArgs a) {
   h8* r2 = pl + 2 * HW;
   h8* r3 = pl + 3 * HW;
   const _Float16* xb = a.x + int64_t(n) * HW * a.xcs + g * 8;
-  for (int p = threadIdx.x; p < HW; p += 256) xs[p] = *reinterpret_cast<const h8*>(xb + int64_t(p) * a.xcs);
+  // plane staging, 4 loads in flight per thread (clamped index; the LDS image is sized HW + 1 so the
+  // out-of-range slot is a dummy and the stores are unconditional)
+  for (int p0 = 0; p0 < HW; p0 += 4 * 256) {
+    h8 v[4];
+    int d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + int(threadIdx.x) + 256 * u;
+      v[u] = *reinterpret_cast<const h8*>(xb + int64_t(min(p, HW - 1)) * a.xcs);
+      d[u] = p < HW ? p : 4 * HW;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pl[d[u]] = v[u];
+  }
   __syncthreads();
   const int r = a.r;
   for (int p = threadIdx.x; p < HW; p += 256) {
@@ -156,7 +169,7 @@ int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y
            x.n, x.h, x.w, x.c, k / 2};
   const int64_t total = int64_t(x.n) * x.h * x.w * (x.c / 8);
   if (total == 0) return FCE_OK;
-  const size_t lds = size_t(4) * x.h * x.w * sizeof(h8);
+  const size_t lds = (size_t(4) * x.h * x.w + 1) * sizeof(h8);  // 4 planes + the staging dummy
   if (lds <= 64 * 1024 && int64_t(x.n) * (x.c / 8) < (int64_t(1) << 31)) {  // H*W <= 1024 (imgsz <= 1024)
     FCE_LAUNCH(maxpool_chain_lds_kernel, dim3(x.n * (x.c / 8)), dim3(256), lds, s, a);
     return launch_status("maxpool_chain_lds_kernel");

@@ -152,20 +152,32 @@ __global__ __launch_bounds__(256) void psa_attention_chunk_kernel(const _Float16
   for (int c0 = 0; c0 < N; c0 += KC) {
     __syncthreads();
     // stage K rows and V^T of keys c0 .. c0 + KC - 1 (zeros past N)
+    // all loads unconditional (clamped key, zero-selected past N) and issued before the LDS stores
+    constexpr int NK = KC * 4 / 256, NV = KC * (HD / 8) / 256;
+    h8 kv[NK], vv[NV];
+    const h8 z8 = h8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < KC * 4 / 256; ++i) {
+    for (int i = 0; i < NK; ++i) {
       const int e = threadIdx.x + 256 * i, key = e >> 2, pc = e & 3;
-      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c0 + key < N) v = *reinterpret_cast<const h8*>(base + int64_t(c0 + key) * qcs + KD + 8 * pc);
-      kl[key * 4 + (pc ^ ((key >> 1) & 3))] = v;
+      const h8 v = *reinterpret_cast<const h8*>(base + int64_t(min(c0 + key, N - 1)) * qcs + KD + 8 * pc);
+      kv[i] = c0 + key < N ? v : z8;
     }
 #pragma unroll
-    for (int i = 0; i < KC * (HD / 8) / 256; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int e = threadIdx.x + 256 * i, key = e / (HD / 8), dc = (e % (HD / 8)) * 8;
-      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c0 + key < N) v = *reinterpret_cast<const h8*>(base + int64_t(c0 + key) * qcs + 2 * KD + dc);
+      const h8 v = *reinterpret_cast<const h8*>(base + int64_t(min(c0 + key, N - 1)) * qcs + 2 * KD + dc);
+      vv[i] = c0 + key < N ? v : z8;
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vt[(dc + j) * VTS + key] = v[j];
+    for (int i = 0; i < NK; ++i) {
+      const int e = threadIdx.x + 256 * i, key = e >> 2, pc = e & 3;
+      kl[key * 4 + (pc ^ ((key >> 1) & 3))] = kv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = threadIdx.x + 256 * i, key = e / (HD / 8), dc = (e % (HD / 8)) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(dc + j) * VTS + key] = vv[i][j];
     }
     __syncthreads();
     const int nt = min(KC, N - c0);
