@@ -168,7 +168,7 @@ def main():
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
     eng = Engine(model, B, S, dev, graph=bool(a.graph))
     nms = NMS(B, eng.anchors, eng.nc, dev)
-    pipe = Pipeline(eng, depth=2)
+    pipe = Pipeline(eng, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")))
 
     def step():
         if a.no_nms:
