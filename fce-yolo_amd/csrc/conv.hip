@@ -981,6 +981,169 @@ static int launch_lds1(const ConvArgs& a0, int out_kind, int rc, int rp, int wp,
   return launch_status("conv1x1_lds_kernel");
 }
 
+// ============================================================================ 1x1, big tiles, K-pipelined
+// For the wide 1x1 convs of the m/l scales (cin, cout >= 64: up to tens of K-steps per output), where
+// conv1x1_lds_kernel's 64-cout blocks re-stage each pixel tile once per cout group and wait on every
+// chunk's loads.  Each wave owns RC=4 cout tiles x RP=4 pixel groups (64 x 64 outputs: 16 MFMAs per
+// K-step per 4 A + 4 B fragment reads); the block (4 waves, WP of them along pixels) owns TPB = WP*64
+// pixels x CBT = (4/WP)*4 cout tiles.  The K loop walks pairs of steps (64 channels): per pair the block
+// stages its B rows (TPB x 128 B, the swizzled image of conv1x1_lds_kernel) and its A fragments (CBT x
+// 2 x 1 KiB, packed order) in one of two LDS buffers with coalesced 16-byte loads, 8 per thread.  Two
+// pairs are in flight in registers: the loads of pair k+2 are issued before pair k's MFMAs, pair k+1's
+// registers are stored to the other buffer after them, one barrier per pair, so each load has two
+// compute phases to land.  Per-output K order (steps 0..nsteps-1) is the implicit-GEMM kernel's:
+// bitwise identical to every other variant.
+template <int WP, int OUT>
+__global__ __launch_bounds__(256, 2) void conv1x1_pipe_kernel(ConvArgs a) {
+  constexpr int RC = 4, RP = 4;
+  constexpr int TPB = WP * RP * 16;
+  constexpr int CBT = (4 / WP) * RC;
+  constexpr int BB = TPB * 8;        // h8 of B per buffer (one pair of steps)
+  constexpr int AB = CBT * 2 * 64;   // h8 of A per buffer
+  constexpr int BUF = BB + AB;
+  constexpr int ITB = BB / 256, ITA = AB / 256, IT = ITB + ITA;
+  static_assert(BB % 256 == 0 && AB % 256 == 0, "whole staging rounds");
+  extern __shared__ __attribute__((aligned(16))) h8 xp[];  // [2][B image | A fragments]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / WP, wp = wave - wc * WP;
+  int bx, by;  // XCD-aware order: a pixel tile's cout groups share an XCD's L2
+  {
+    const int total = a.gx * a.gy, b = blockIdx.x;
+    const int per = total >> 3, body = per << 3;
+    const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+    bx = L / a.gy;
+    by = L - bx * a.gy;
+  }
+  const int pix0 = bx * TPB;
+  const int cbl0 = by * CBT;
+  const int cotiles = (a.cout + 15) >> 4;
+  // staging pieces: B piece e = threadIdx.x + 256 i -> pixel e >> 3, 16-byte piece j = e & 7 of its
+  // 128-byte pair; A piece e -> cout tile e >> 7, step (e >> 6) & 1, lane e & 63 (2 KiB per tile)
+  const h8* sptr[IT];
+  int spos[IT], sch[ITB];
+  bool spv[ITB];
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int j = e & 7, p = e >> 3;
+    const int pix = pix0 + p;
+    spv[i] = pix < a.P;
+    sptr[i] = reinterpret_cast<const h8*>(a.x + conv1x1_src(a, spv[i] ? pix : 0) + j * 8);
+    sch[i] = j * 8;
+    spos[i] = p * 8 + (j ^ ((p >> 1) & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < ITA; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int t = e >> 7, sl = e & 127;  // sl = step * 64 + lane
+    sptr[ITB + i] = reinterpret_cast<const h8*>(a.w) + size_t(min(cbl0 + t, cotiles - 1)) * a.nalloc * 64 + sl;
+    spos[ITB + i] = BB + e;
+  }
+  auto load = [&](int k0, h8 (&v)[IT]) {  // packed A is zero-padded past nsteps: in bounds
+    const int cbase = k0 * 32;
+#pragma unroll
+    for (int i = 0; i < ITB; ++i) {
+      const bool ok = spv[i] && cbase + sch[i] < a.cin;
+      v[i] = *(ok ? sptr[i] + cbase / 8 : reinterpret_cast<const h8*>(g_zero_line));
+    }
+#pragma unroll
+    for (int i = 0; i < ITA; ++i) v[ITB + i] = sptr[ITB + i][size_t(k0) * 64];
+  };
+  auto store = [&](int buf, const h8 (&v)[IT]) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) xp[buf * BUF + spos[i]] = v[i];
+  };
+  f4 acc[RC][RP];
+#pragma unroll
+  for (int r = 0; r < RC; ++r)
+#pragma unroll
+    for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  const int pw = wp * RP * 16;
+  const int npair = (a.nsteps + 1) >> 1;
+  h8 v0[IT], v1[IT];
+  load(0, v0);
+  if (npair > 1) load(2, v1);
+  store(0, v0);
+  __syncthreads();
+  for (int k = 0; k < npair; ++k) {
+    const int cur = k & 1;
+    if (k + 2 < npair) load(2 * (k + 2), v0);  // v0 was stored last iteration
+    const int nsc = min(2, a.nsteps - 2 * k);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s < nsc) {
+        h8 af[RC], bf[RP];
+#pragma unroll
+        for (int r = 0; r < RC; ++r) af[r] = xp[cur * BUF + BB + ((wc * RC + r) * 2 + s) * 64 + lane];
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int px = pw + p * 16 + col;
+          const int j = s * 4 + grp;
+          bf[p] = xp[cur * BUF + px * 8 + (j ^ ((px >> 1) & 7))];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+          for (int p = 0; p < RP; ++p)
+            acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+      }
+    }
+    if (k + 1 < npair) store(cur ^ 1, v1);
+    __syncthreads();  // pair k's reads and pair k+1's stores done
+#pragma unroll
+    for (int i = 0; i < IT; ++i) v1[i] = v0[i];
+  }
+  if constexpr (OUT == OUT_F16 || OUT == OUT_WSTORE) {
+    if (a.stg) {  // launch_pipe1 sizes the LDS for the output tile too (TPB x CBT*16 couts x 2 bytes)
+      conv_store_staged<RC, RP, CBT, TPB, OUT>(a, acc, pix0, pw, cbl0, wc, col, grp, reinterpret_cast<_Float16*>(xp));
+      return;
+    }
+  }
+  conv_epilogue<RC, RP, OUT>(a, acc, pix0 + pw, cbl0 + wc * RC, col, grp);
+}
+
+// big-tile configurations, coded 0x700 | log2(wp) << 12 (rc = rp = 4)
+static bool pipe1_ok(const fce_conv_desc& d, int det_box) {
+  return d.k == 1 && d.stride == 1 && !det_box && d.cout >= 64 && d.cin >= 64;
+}
+
+template <int WP>
+static int launch_pipe1_w(const ConvArgs& a, int out_kind, dim3 grid, size_t lds, hipStream_t s) {
+#define PIPE1_L(O)                                                                                      \
+  {                                                                                                     \
+    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_pipe_kernel<WP, O>), \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024) == hipSuccess; \
+    FCE_CHECK(lds_ok || lds <= 64 * 1024, "conv 1x1 big tile: cannot opt in to >64 KiB LDS");          \
+    FCE_LAUNCH((conv1x1_pipe_kernel<WP, O>), grid, dim3(256), lds, s, a);                               \
+  }
+  switch (out_kind) {
+    case OUT_F16: PIPE1_L(OUT_F16); break;
+    case OUT_F32: PIPE1_L(OUT_F32); break;
+    case OUT_WSTORE: PIPE1_L(OUT_WSTORE); break;
+    case OUT_CLS: PIPE1_L(OUT_CLS); break;
+    default: PIPE1_L(OUT_ACCUM); break;
+  }
+#undef PIPE1_L
+  return FCE_OK;
+}
+
+static int launch_pipe1(const ConvArgs& a0, int out_kind, int wp, hipStream_t s) {
+  FCE_CHECK(out_kind != OUT_DFL && (wp == 1 || wp == 2 || wp == 4), "conv 1x1 big tile: bad configuration");
+  ConvArgs a = a0;
+  const int cotiles = (a.cout + 15) / 16, cb = (4 / wp) * 4, tpb = wp * 64;
+  a.gx = (a.P + tpb - 1) / tpb;
+  a.gy = (cotiles + cb - 1) / cb;
+  FCE_CHECK(int64_t(a.gx) * a.gy < (int64_t(1) << 31), "conv 1x1 big tile: grid too large");
+  const size_t lds = std::max(size_t(2) * (tpb * 128 + cb * 2048), a.stg ? size_t(tpb) * cb * 16 * 2 : size_t(0));
+  const dim3 grid(unsigned(a.gx * a.gy));
+  const int st = wp == 1 ? launch_pipe1_w<1>(a, out_kind, grid, lds, s)
+                 : wp == 2 ? launch_pipe1_w<2>(a, out_kind, grid, lds, s)
+                           : launch_pipe1_w<4>(a, out_kind, grid, lds, s);
+  if (st != FCE_OK) return st;
+  return launch_status("conv1x1_pipe_kernel");
+}
+
 // ============================================================================ 3x3, LDS halo tiles
 // For cin % 32 == 0.  A block (4 waves) owns a 2-D output tile of TW = 16 columns x TH = 4*RP rows
 // of one image and RC*16 couts; wave w owns rows [w*RP, w*RP+RP) (one 16-pixel B fragment per row).
@@ -2227,6 +2390,12 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
           if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
           if (n < cap) out[n++] = 0x500 | rc | (rp << 4) | (wl << 12);
         }
+  if (pipe1_ok(d, det_box))  // big-tile K-pipelined 1x1: 0x700 | log2(wp) << 12
+    for (int wl = 0; wl < 3; ++wl) {
+      const int cb = (4 >> wl) * 4;
+      if ((cb >> 1) >= cotiles) continue;
+      if (n < cap) out[n++] = 0x700 | (wl << 12);
+    }
   if (d.k == 3 && d.cin % 32 != 0 && d.cin <= 64 && d.up == 0 && !det_box)  // small-cin LDS tile: 0x200 | ..
     for (int rc : {1, 2, 4}) {
       if (rc > 1 && (rc >> 1) >= cotiles) continue;
@@ -2566,6 +2735,11 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     FCE_CHECK(d.k == 1 && d.stride == 1 && ring_ok(g.nsteps, rc, rp, wp), "conv: bad 1x1 ring hint");
     if (out_kind == OUT_DFL) FCE_CHECK(rc == 4 && wp == 4 && g.cotiles == 4, "conv detect epilogue: one wave must own all 64 bins");
     return launch_ring(a, out_kind, rc, rp, wp, s);
+  }
+  if (kind == 7) {  // big-tile K-pipelined 1x1 kernel
+    const int wp = 1 << ((tile >> 12) & 3);
+    FCE_CHECK(pipe1_ok(d, out_kind == OUT_DFL) && (tile & 0xFF) == 0 && wp <= 4, "conv: bad big-tile 1x1 hint");
+    return launch_pipe1(a, out_kind, wp, s);
   }
   if (kind == 4) {  // LDS-staged 1x1 kernel
     rc = tile & 15;

@@ -2,7 +2,7 @@
 
     python scripts/tune_report.py [--model yolo11n-fce.yaml] [--batch 32] [--imgsz 640] > report.txt
 Variant codes: rc | rp << 4 (implicit GEMM), 0x100 | .. (3x3 LDS tile, cin % 32 == 0), 0x200 | ..
-(3x3 LDS tile, small cin), 0x300 | .. (1x1 streaming), 0x400 | .. | log2(wp) << 12 (1x1 LDS tile), 0x500 (1x1 ring),
+(3x3 LDS tile, small cin), 0x300 | .. (1x1 streaming), 0x400 | .. | log2(wp) << 12 (1x1 LDS tile), 0x500 (1x1 ring), 0x700 | log2(wp) << 12 (1x1 big tile, K-pipelined),
 100 + v (depthwise variant v).
 """
 import argparse

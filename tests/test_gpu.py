@@ -266,6 +266,8 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (576, 256, 1, 1, 5, 7, False), (32, 32, 1, 1, 256, 256, False), (64, 48, 1, 1, 200, 200, True),
     (192, 128, 1, 1, 128, 160, False), (32, 64, 3, 2, 90, 100, False), (64, 48, 3, 1, 130, 70, True),
     (64, 80, 3, 2, 41, 37, False),
+    # wide 1x1s of the m/l scales (big-tile K-pipelined kernel, 0x7xx): odd K-step counts, partial cout tiles
+    (512, 256, 1, 1, 40, 40, True), (96, 256, 1, 1, 33, 35, False), (136, 72, 1, 1, 19, 23, True),
 ]
 
 
@@ -302,6 +304,7 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
     codes = (C.c_int * 128)()
     nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     assert any((codes[i] & 0xF00) == 0x400 for i in range(nv))
+    assert any((codes[i] & 0xF00) == 0x700 for i in range(nv)) == (cin >= 64 and cout >= 64)
     outs = {}
     for code in [-1] + list(codes[:nv]):
         y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
