@@ -721,12 +721,17 @@ static int autotune(fce_net* net) {
       op.tile = cand[i];
       for (int r = 0; r < 2 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
       if (st) break;
-      (void)hipEventRecord(e0, ts);
-      for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
-      (void)hipEventRecord(e1, ts);
-      if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, e0, e1);
+      // best of two 3-launch windows: one window alone let clock / co-tenant noise flip close picks
+      float ms = 1e30f;
+      for (int t = 0; t < 2 && st == FCE_OK; ++t) {
+        (void)hipEventRecord(e0, ts);
+        for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
+        (void)hipEventRecord(e1, ts);
+        if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
+        float w = 0.f;
+        (void)hipEventElapsedTime(&w, e0, e1);
+        ms = std::min(ms, w);
+      }
       if (st == FCE_OK) net->tune_log.push_back({int(&op - net->ops.data()), cand[i], ms / 3.f});
       if (st == FCE_OK && ms < best_ms) {
         best_ms = ms;
