@@ -13,4 +13,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   [ $rc -eq 0 ] || exit $rc
 done
 python scripts/pmc_summary.py gpurun_out/pmc/${TAG}_FETCH_SIZE gpurun_out/pmc/${TAG}_WRITE_SIZE gpurun_out/pmc/${TAG}_profile_FETCH_SIZE.json > gpurun_out/pmc/${TAG}_summary.json
-rc=$?; tail -c 1500 gpurun_out/pmc/${TAG}_summary.json; exit $rc
+rc=$?; tail -c 600 gpurun_out/pmc/${TAG}_summary.json
+# the raw per-dispatch CSVs of a large model exceed what gpurun copies back: keep the summary only
+rm -rf gpurun_out/pmc/${TAG}_FETCH_SIZE gpurun_out/pmc/${TAG}_WRITE_SIZE
+exit $rc
