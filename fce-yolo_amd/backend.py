@@ -1,9 +1,11 @@
-"""Two backends for the same module lowering (``Module.emit(be, x, out=None)``):
+"""Backends for the same module lowering (``Module.emit(be, x, out=None)``):
 
 * ``EagerBackend`` — drop-in mode: each op runs immediately through the C-ABI on torch-allocated
   channels_last fp16 buffers on the current HIP stream (what ``nn.Module.forward`` uses).
 * ``NetBackend``  — whole-graph mode: each op is recorded into a native ``fce_net`` (buffer
   arena + launch list, hipGraph replay).  The Python side only lowers once.
+* ``ShapeBackend`` — shape propagation only (``meta`` tensors out) for non-ROCm inputs, such as
+  the reference's CPU stride probe while it builds a model.
 
 A ``View`` is an NHWC channel slice [coff, coff+c) of a buffer with ``cstride`` channels, at
 logical size (h, w); ``up`` > 0 marks a lazily nearest-upsampled view of a (h>>up, w>>up) buffer
@@ -57,6 +59,7 @@ def _fusion(fusion):
 class EagerBackend:
     """Runs every op immediately (drop-in nn.Module path)."""
 
+    shape_only = False
     def __init__(self, device: torch.device):
         self.device = device
         self.stream = torch.cuda.current_stream(device).cuda_stream
@@ -154,6 +157,37 @@ class EagerBackend:
         return out
 
 
+class ShapeBackend:
+    """Shape propagation only: no device, no data, no arithmetic.
+
+    This is the drop-ins' answer to a non-ROCm input, e.g. the CPU ``torch.zeros(1, ch, 256, 256)``
+    stride probe that the reference runs while building a model (``tasks.py:396-411``). Outputs are
+    ``meta`` tensors of the reference's output shape: anything that reads their values fails loudly, so
+    this is never a numeric CPU fallback."""
+
+    shape_only = True
+    fused_detect = False
+    device = torch.device("meta")
+
+    def alloc(self, n, c, h, w, dtype=N.F16) -> View:
+        return View(None, n, c, h, w, c, 0, dtype)
+
+    def from_torch(self, x: torch.Tensor, keep_nchw: bool = False) -> View:
+        n, c, h, w = x.shape
+        return View(None, n, c, h, w, c, 0, N.F16, N.NCHW if keep_nchw else N.NHWC)
+
+    def to_torch(self, v: View, dtype=torch.float16) -> torch.Tensor:
+        return torch.empty((v.n, v.c, v.h, v.w), dtype=dtype, device="meta")
+
+    def materialize(self, v: View) -> View:
+        return self.alloc(v.n, v.c, v.h, v.w) if v.up else v
+
+    def conv(self, *a, **k):
+        pass
+
+    maxpool_chain = wadd = coord = psa = conv_detect = conv
+
+
 class _OneCache:
     def __init__(self):
         self.t = {}
@@ -171,6 +205,7 @@ class NetBackend:
     """Records ops into a native fce_net for an input of logical size (H, W)."""
 
     fused_detect = True  # Detect tail fused into the last convs' epilogues (no fp32 maps)
+    shape_only = False
 
     def __init__(self, H: int, W: int, device: torch.device):
         self.H, self.W = H, W

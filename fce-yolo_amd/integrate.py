@@ -27,6 +27,8 @@ def from_reference_model(ref_model, device=None) -> DetectionModel:
     yaml_d = {k: v for k, v in dict(ref_model.yaml).items() if k != "yaml_file"}
     model = DetectionModel(yaml_d)
     sd = {k: (v.float() if v.is_floating_point() else v) for k, v in ref_model.state_dict().items()}
+    if not any(".bn." in k for k in sd) and not model.is_fused():
+        model.fuse()  # AutoBackend fuses by default (autobackend.py:203-207): mirror the fused layout
     model.load_state_dict(sd)
     model.names = dict(getattr(ref_model, "names", model.names))
     model.eval()
@@ -64,13 +66,15 @@ def device_postprocess(predictor):
     orig = nms_mod.non_max_suppression
 
     def nms(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False, multi_label=False,
-            labels=(), max_det=300, nc=0, max_time_img=0.05, max_nms=30000, max_wh=7680, in_place=True,
-            rotated=False, end2end=False, return_idxs=False):
+            labels=(), max_det=300, nc=0, max_time_img=0.05, max_nms=30000, max_wh=7680, rotated=False,
+            end2end=False, return_idxs=False):
+        """The signature of utils/nms.py:13-29; argument combinations off the device path go to `orig`."""
         pred = prediction[0] if isinstance(prediction, (list, tuple)) else prediction
-        if (classes is not None or agnostic or multi_label or labels or nc or rotated or end2end
+        if (classes is not None or agnostic or multi_label or len(labels) or nc or rotated or end2end
                 or pred.device.type != "cuda"):
-            return orig(prediction, conf_thres, iou_thres, classes, agnostic, multi_label, labels, max_det, nc,
-                        max_time_img, max_nms, max_wh, in_place, rotated, end2end, return_idxs)
+            return orig(prediction, conf_thres=conf_thres, iou_thres=iou_thres, classes=classes, agnostic=agnostic,
+                        multi_label=multi_label, labels=labels, max_det=max_det, nc=nc, max_time_img=max_time_img,
+                        max_nms=max_nms, max_wh=max_wh, rotated=rotated, end2end=end2end, return_idxs=return_idxs)
         return non_max_suppression(pred, conf_thres, iou_thres, max_det, max_nms, max_wh, return_idxs)
 
     nms_mod.non_max_suppression = nms

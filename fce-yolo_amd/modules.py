@@ -6,7 +6,9 @@ resolves module names to these classes (reference ``ultralytics/nn/tasks.py:1582
 reference checkpoints' state_dicts load unchanged.  ``forward`` runs the HIP kernels through the
 C-ABI (eager drop-in mode, NCHW-logical / NHWC-physical channels_last tensors); ``emit`` lowers the
 same computation onto a backend (see ``backend.py``), which is how the whole-graph executor is
-built.  There is no CPU path: a CPU tensor raises.
+built.  There is no CPU arithmetic: a non-ROCm input only propagates shapes and returns ``meta``
+tensors (``ShapeBackend``), which is what the reference's CPU stride probe at model construction
+needs (``tasks.py:396-411``) and fails loudly wherever values are read.
 
 BatchNorm eps is 1e-3 (reference ``utils/torch_utils.py:470`` sets it for every model; Q4), and
 BN is folded into the conv at first use exactly like ``fuse_conv_and_bn`` (torch_utils.py:237-267).
@@ -22,7 +24,7 @@ import torch
 import torch.nn as nn
 
 from . import _native as N
-from .backend import EagerBackend, View
+from .backend import EagerBackend, ShapeBackend, View
 
 BN_EPS = 1e-3
 
@@ -70,6 +72,24 @@ def fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d | None):
             w = (w.view(w.shape[0], -1) * s[:, None]).view(w.shape)
             b = s * b + (beta - g * mean / torch.sqrt(var + bn.eps))
     return w, b
+
+
+def fuse_conv_bn(m: "Conv") -> None:
+    """One step of ``BaseModel.fuse`` (tasks.py:231-237) with ``fuse_conv_and_bn`` (torch_utils.py:237-267):
+    BN folded into ``conv.weight`` / ``conv.bias`` (eps 1e-3), ``bn`` deleted, forward -> forward_fuse.
+    The kernels fold BN themselves, so this only changes the module's state_dict layout (a fused
+    checkpoint loads after it)."""
+    w, b = fold_bn(m.conv, m.bn)
+    conv = m.conv
+    with torch.no_grad():
+        conv.weight.data = w.to(conv.weight.dtype)
+        if conv.bias is None:
+            conv.register_parameter("bias", nn.Parameter(b.to(conv.weight.dtype)))
+        else:
+            conv.bias.data = b.to(conv.bias.dtype)
+    conv.requires_grad_(False)
+    del m.bn
+    m.forward = m.forward_fuse
 
 
 def pack_conv(desc: N.ConvDesc, w: torch.Tensor, device) -> torch.Tensor:
@@ -123,12 +143,14 @@ def _desc_copy(d: N.ConvDesc, **kw) -> N.ConvDesc:
 
 def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = None, res: View | None = None,
               epilogue: int = N.EPI_STORE, fusion=None, out_dtype=N.F16) -> View:
-    nat = conv_native(conv, bn, act, be.device)
     k, s = conv.kernel_size[0], conv.stride[0]
     ho = (x.h + 2 * (k // 2) - k) // s + 1
     wo = (x.w + 2 * (k // 2) - k) // s + 1
     y = out if out is not None else be.alloc(x.n, conv.out_channels, ho, wo, out_dtype)
     assert (y.h, y.w, y.c) == (ho, wo, conv.out_channels), "output view mismatch"
+    if be.shape_only:
+        return y
+    nat = conv_native(conv, bn, act, be.device)
     fw, fn, fi = fusion if fusion is not None else (None, 0, 0)
     desc = _desc_copy(nat.desc, epilogue=epilogue, fusion_w=fw, fusion_n=fn, fusion_i=fi)
     if x.layout == N.NCHW and conv.in_channels > 4:
@@ -139,13 +161,21 @@ def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = No
     return y
 
 
+def _backend(xs):
+    """EagerBackend for ROCm inputs; ShapeBackend (meta outputs, no arithmetic) for anything else."""
+    devs = {t.device.type for t in xs}
+    if devs == {"cuda"}:
+        return EagerBackend(xs[0].device)
+    if "cuda" in devs:
+        raise RuntimeError(f"fce_yolo_amd: inputs on mixed devices {sorted(devs)}")
+    return ShapeBackend()
+
+
 def _run_eager(mod, x, *, keep_nchw=False, out_dtype=None):
-    """Drop-in forward: NCHW tensor(s) in, channels_last tensor out (input dtype preserved)."""
+    """Drop-in forward: NCHW tensor(s) in, channels_last tensor out (input dtype preserved).  A non-ROCm
+    input gives a ``meta`` tensor of the output shape (see ``ShapeBackend``), never CPU arithmetic."""
     xs = x if isinstance(x, (list, tuple)) else [x]
-    dev = xs[0].device
-    if dev.type != "cuda":
-        raise RuntimeError(f"{type(mod).__name__}: fce_yolo_amd runs on ROCm devices only (got {dev}); no CPU fallback")
-    be = EagerBackend(dev)
+    be = _backend(xs)
     views = [be.from_torch(t, keep_nchw=keep_nchw) for t in xs]
     y = mod.emit(be, views if isinstance(x, (list, tuple)) else views[0])
     dt = out_dtype or xs[0].dtype
@@ -181,7 +211,8 @@ class Conv(nn.Module):
         return _run_eager(self, x, keep_nchw=self.conv.in_channels <= 4)
 
     def forward_fuse(self, x):
-        return self.forward(x)
+        """BaseModel.fuse (tasks.py:231-237) rebinds ``forward`` to this; BN folding is in conv_native."""
+        return _run_eager(self, x, keep_nchw=self.conv.in_channels <= 4)
 
 
 class DWConv(Conv):
@@ -355,8 +386,9 @@ class Attention(nn.Module):
     def emit(self, be, x, out=None, res=None):
         qkv = self.qkv.emit(be, x)
         o = be.alloc(x.n, self.num_heads * self.head_dim, x.h, x.w)
-        pw, pb = self._pe(be.device)
-        be.psa(qkv, self.num_heads, self.key_dim, self.head_dim, pw.data_ptr(), pb.data_ptr(), o)
+        if not be.shape_only:
+            pw, pb = self._pe(be.device)
+            be.psa(qkv, self.num_heads, self.key_dim, self.head_dim, pw.data_ptr(), pb.data_ptr(), o)
         return self.proj.emit(be, o, out=out, res=res)
 
     def forward(self, x):
@@ -430,7 +462,7 @@ class BiFPN_Concat(nn.Module):
     def emit(self, be, xs, out=None):
         h, w = xs[0].h, xs[0].w
         y = out if out is not None else be.alloc(xs[0].n, self.output_ch, h, w)
-        wp = self._w32(be.device).data_ptr()
+        wp = None if be.shape_only else self._w32(be.device).data_ptr()
         n = len(xs)
         for i, (x, m) in enumerate(zip(xs, self.realign_convs)):
             assert (x.h, x.w) == (h, w), "BiFPN_Concat inputs must share the spatial size"
@@ -482,6 +514,8 @@ class CoordAtt(nn.Module):
 
     def emit(self, be, x, out=None):
         inp, mip, oup = self.cv1.conv.in_channels, self.cv1.conv.out_channels, self.cv_h.out_channels
+        if be.shape_only:
+            return out if out is not None else be.alloc(x.n, oup, x.h, x.w)
 
         def build():
             w, b = fold_bn(self.cv1.conv, getattr(self.cv1, "bn", None))
@@ -519,6 +553,8 @@ class CoordCrossAtt(nn.Module):
         inp, oup = self.cv1.in_channels, self.proj.out_channels
         if inp != oup:
             raise RuntimeError("CoordCrossAtt: oup != inp cannot broadcast x * y_att (reference fce_block.py:180)")
+        if be.shape_only:
+            return out if out is not None else be.alloc(x.n, oup, x.h, x.w)
         mats = [_dense(m, be.device) for m in (self.cv1, self.q_conv, self.k_conv, self.v_conv, self.proj)]
         d = _coord_desc(inp, oup, self.mip, self.num_heads, self.scale, mats, None, be.device)
         y = out if out is not None else be.alloc(x.n, oup, x.h, x.w)
@@ -553,6 +589,8 @@ class BiCoordCrossAtt(nn.Module):
 
     def emit(self, be, x, out=None):
         inp, oup = self.proj_q_h.in_channels, self.out_h.out_channels
+        if be.shape_only:
+            return out if out is not None else be.alloc(x.n, oup, x.h, x.w)
         mods = (self.proj_q_h, self.proj_k_h, self.proj_v_h, self.proj_q_w, self.proj_k_w, self.proj_v_w,
                 self.out_h, self.out_w)
         d = _coord_desc(inp, oup, self.mid_dim, self.num_heads, self.scale, [_dense(m, be.device) for m in mods],
@@ -578,13 +616,21 @@ class DFL(nn.Module):
 
 
 class Detect(nn.Module):
-    """head.py:26-167 (legacy=False cls branch, Q5).  Inference returns (y, maps)."""
+    """head.py:26-212 (legacy=False cls branch, Q5).
+
+    Eval mode returns ``(y, maps)`` and train mode the raw ``maps`` list, as ``head.py:114-124`` does;
+    the reference's stride probe (``tasks.py:396-411``) runs train mode on a CPU tensor, which goes
+    through ``ShapeBackend`` (meta maps of the right shapes).  ``anchors`` / ``strides`` are the
+    reference's class-level tensors, so ``BaseModel._apply`` (``tasks.py:276-293``) can move them."""
 
     dynamic = False
     export = False
+    format = None
     end2end = False
     max_det = 300
     shape = None
+    anchors = torch.empty(0)
+    strides = torch.empty(0)
     legacy = False
     xyxy = False
 
@@ -613,11 +659,17 @@ class Detect(nn.Module):
         )
         self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
 
-    def strides(self):
+    def level_strides(self) -> list[float]:
         s = [float(v) for v in self.stride]
         if not all(s):
             raise RuntimeError("Detect.stride is not set (DetectionModel sets [8, 16, 32])")
         return s
+
+    def bias_init(self):
+        """head.py:169-180 (box bias 1, cls bias log(5 / nc / (640 / s)^2)); needs the strides."""
+        for a, b, s in zip(self.cv2, self.cv3, self.stride):
+            a[-1].bias.data[:] = 1.0
+            b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / s) ** 2)
 
     def _branches(self, be, x, i):
         """Features feeding the last 1x1 convs of level i: (box branch, cls branch)."""
@@ -633,25 +685,37 @@ class Detect(nn.Module):
     def _finals(self, i):
         return ((0, self.cv2[i][2]), (1, self.cv3[i][2]))
 
+    def _raw_map(self, be, feats, i):
+        """cat(cv2[i](x), cv3[i](x)) as one fp32 (B, no, h, w) buffer (head.py:118)."""
+        b, c = feats
+        mp = be.alloc(b.n, self.no, b.h, b.w, N.F32)
+        emit_conv(be, self.cv2[i][2], None, False, b, out=mp.slice(0, 4 * self.reg_max))
+        emit_conv(be, self.cv3[i][2], None, False, c, out=mp.slice(4 * self.reg_max, self.nc))
+        return mp
+
+    def emit_maps(self, be, xs):
+        """Train-mode head (head.py:118-120): the raw maps only, no decode (strides not needed)."""
+        return [self._raw_map(be, self._branches(be, x, i), i) for i, x in enumerate(xs)]
+
     def emit(self, be, xs, out=None):
         """Graph backend: the box / cls logits never leave the last convs (fp32 DFL decode + sigmoid in
         the epilogue, written straight into pred).  Eager backend: the same fused kernels produce pred
         (bit-identical to the graph path) and fp32 raw maps are also written for the reference's
         ``(y, x)`` return (head.py:122-124)."""
-        strides = self.strides()
         fused_only = getattr(be, "fused_detect", False)
+        A = sum(v.h * v.w for v in xs)
+        if be.shape_only:
+            pred = torch.empty((xs[0].n, 4 + self.nc, A), dtype=torch.float32, device="meta")
+            return pred, self.emit_maps(be, xs)
+        strides = self.level_strides()
         pred, maps = None, []
         if not fused_only:
-            A = sum(v.h * v.w for v in xs)
             pred = torch.empty((xs[0].n, 4 + self.nc, A), dtype=torch.float32, device=be.device)
         off = 0
         for i, x in enumerate(xs):
             feats = self._branches(be, x, i)
             if not fused_only:
-                mp = be.alloc(x.n, self.no, x.h, x.w, N.F32)  # cat(box, cls) raw logits, fp32
-                emit_conv(be, self.cv2[i][2], None, False, feats[0], out=mp.slice(0, 4 * self.reg_max))
-                emit_conv(be, self.cv3[i][2], None, False, feats[1], out=mp.slice(4 * self.reg_max, self.nc))
-                maps.append(mp)
+                maps.append(self._raw_map(be, feats, i))
             for (part, conv), v in zip(self._finals(i), feats):
                 nat = conv_native(conv, None, False, be.device)
                 if fused_only:
@@ -665,10 +729,9 @@ class Detect(nn.Module):
 
     def forward(self, x):
         xs = list(x)
-        dev = xs[0].device
-        if dev.type != "cuda":
-            raise RuntimeError("Detect: fce_yolo_amd runs on ROCm devices only; no CPU fallback")
-        be = EagerBackend(dev)
+        be = _backend(xs)
         views = [be.from_torch(t) for t in xs]
+        if self.training:
+            return [be.to_torch(m, torch.float32) for m in self.emit_maps(be, views)]
         pred, maps = self.emit(be, views)
         return pred, [be.to_torch(m, torch.float32) for m in maps]

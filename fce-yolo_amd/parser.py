@@ -211,6 +211,14 @@ class DetectionModel(nn.Module):
         pred, maps = self.emit(be, be.from_torch(x, keep_nchw=True))
         return pred, [be.to_torch(m, torch.float32) for m in maps]
 
+    def is_fused(self) -> bool:
+        return not any(isinstance(m, nn.BatchNorm2d) for m in self.modules())
+
     def fuse(self, verbose=False):
-        """BN is folded when the native weights are built; kept for API compatibility (tasks.py:223)."""
+        """tasks.py:223-252: fold every Conv / DWConv BN into its conv (eps 1e-3) and drop the BN.  The
+        kernels fold BN when they pack weights, so a fused and an unfused model compute the same; this
+        gives the fused state_dict layout (``*.conv.bias``, no ``*.bn.*``) that AutoBackend's models have."""
+        for m in self.model.modules():
+            if isinstance(m, M.Conv) and hasattr(m, "bn"):
+                M.fuse_conv_bn(m)
         return self

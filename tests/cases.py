@@ -128,3 +128,66 @@ def oracle_model(model, x, dtype=torch.float64):
     with torch.no_grad():
         return O.forward(layers, save, {"model." + k[len("model."):] if k.startswith("model.") else k: v
                                         for k, v in sd.items()}, x.to(dtype))
+
+
+# ---------------------------------------------------------------- BASELINE-size fixtures (golden/full.npz)
+FULL = {
+    # fixture key: (cfg, mutate, batch, imgsz) -- make_golden_full.E2E_FULL
+    "yolo11n-fce_640_b2": ("yolo11n-fce.yaml", None, 2, 640),
+    "yolo11s-bifpn_640_b1": ("yolo11s-bifpn.yaml", None, 1, 640),
+    "yolo11l-fce_640_b1": ("yolo11l-fce.yaml", None, 1, 640),
+    "yolo11m-fce-h8_1280_b1": ("yolo11m-fce.yaml", heads8, 1, 1280),
+}
+OPS_FULL = {
+    # fixture key: (module class, ctor args, input shape) -- make_golden_full.OPS_FULL
+    "bicoord_n_80": (M.BiCoordCrossAtt, (128, 128, 8, 4), (2, 128, 80, 80)),
+    "bicoord_l_80": (M.BiCoordCrossAtt, (512, 512, 8, 4), (1, 512, 80, 80)),
+    "bicoord_m_160": (M.BiCoordCrossAtt, (512, 512, 8, 8), (1, 512, 160, 160)),
+    "c2psa_m_40": (M.C2PSA, (512, 512, 1), (1, 512, 40, 40)),
+    "c2psa_n_20": (M.C2PSA, (256, 256, 1), (2, 256, 20, 20)),
+}
+
+
+def full_input(key, fx):
+    _, _, b, s = FULL[key]
+    return torch.rand(b, 3, s, s, generator=torch.Generator().manual_seed(int(fx["x_seed"])))
+
+
+def full_op(key, fx):
+    """(module with the fixture's seeded weights, input) of a BASELINE-size per-op fixture."""
+    cls, args, shape = OPS_FULL[key]
+    mod = cls(*args)
+    mod.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in mod.state_dict().items()], int(fx["seed"])))
+    for m in mod.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eps = 1e-3
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(int(fx["x_seed"])))
+    return mod.eval(), x
+
+
+def full_op_oracle(key, mod, x, dtype=torch.float32):
+    cls, args, _ = OPS_FULL[key]
+    sd = O.cast_sd(O.fuse_state_dict({"m." + k: v for k, v in mod.state_dict().items()}), dtype)
+    with torch.no_grad():
+        if cls is M.C2PSA:
+            return O.c2psa(sd, "m", x.to(dtype), list(args))
+        return O.bicoordcrossatt(sd, "m", x.to(dtype), list(args))
+
+
+def op_slice(y):
+    """make_golden_full.op_slice."""
+    return y[:, ::3, ::5, ::7]
+
+
+def compare_full(y, fx, anchors=True):
+    """Errors of a full output against a BASELINE-size fixture: (slice error, row-sum error), both relative
+    to max|ref slice| (row sums: relative to the row's sum of |values| bound A * max|ref|)."""
+    y = y.double().cpu()
+    ref = torch.from_numpy(fx["slice"]).double()
+    ys = y[:, :, ::37] if anchors else op_slice(y)
+    scale = ref.abs().max().clamp_min(1e-12)
+    e_slice = ((ys - ref).abs().max() / scale).item()
+    sums = y.sum(dim=2) if anchors else y.sum(dim=(2, 3))
+    n = y.shape[2] if anchors else y.shape[2] * y.shape[3]
+    e_sum = ((sums - torch.from_numpy(fx["sum"])).abs().max() / (scale * n)).item()
+    return e_slice, e_sum

@@ -48,6 +48,11 @@ def e2e_fx():
 
 
 @pytest.fixture(scope="session")
+def full_fx():
+    return _Npz(GOLDEN / "full.npz")
+
+
+@pytest.fixture(scope="session")
 def nms_fx():
     return _Npz(GOLDEN / "nms.npz")
 

@@ -137,6 +137,73 @@ def test_graph_eager_and_module_forward_agree_bitwise(e2e_fx, device, monkeypatc
     assert torch.equal(yg, ye) and torch.equal(yg, yg2) and torch.equal(yg, ym) and torch.equal(yg, ys)
 
 
+def _predict_once(model, x):
+    """tasks.py:160-188 as the reference runs it with the drop-ins bound: module by
+    module through ``forward``; ``nn.Upsample`` is torch's own there, so it runs as torch's here."""
+    y = []
+    for m in model.model:
+        if m.f != -1:
+            x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+        x = torch.nn.Upsample.forward(m, x) if isinstance(m, M.Upsample) else m(x)
+        y.append(x if m.i in model.save else None)
+    return x
+
+
+@pytest.mark.parametrize("key", list(cases.E2E))
+def test_dropin_predict_once_parity(key, e2e_fx, device):
+    """The eager drop-in path the reference drives: fuse() (tasks.py:223-252, restated by
+    DetectionModel.fuse and checked against the reference in test_reference_dropin.py), .half().to(cuda),
+    eval, per-module forward -> (y, maps); y against the reference's fused fp32 output."""
+    fx = e2e_fx.group(key)
+    cfg, mut = cases.E2E[key]
+    model = cases.seeded_model(cfg, 0, mut).fuse().half().to(device).eval()
+    x = cases.e2e_input(key, fx)
+    with torch.inference_mode():
+        y, maps = _predict_once(model, x.half().to(device))
+    ref = torch.from_numpy(fx["y"])
+    assert y.shape == ref.shape and len(maps) == 3 and torch.isfinite(y).all()
+    box = _rel(y[:, :4], ref[:, :4])
+    cls = (y[:, 4:].cpu() - ref[:, 4:]).abs().max().item()
+    print(f"{key}: drop-in box rel {box:.2e} cls abs {cls:.2e}")
+    assert box <= BOX_TOL and cls <= CLS_TOL, (box, cls)
+
+
+@pytest.mark.parametrize("key", list(cases.FULL))
+def test_full_size_parity(key, full_fx, device):
+    """BASELINE configs at their real sizes (m-h8 @1280: C2PSA over 1600 keys, BiCoord L5 at 160x160 on the
+    >64 KiB LDS path; l / s @640; n @640 bs2): the whole output against the oracle (fp32, run on this
+    host) and the reference's slices / row sums (golden/full.npz)."""
+    fx = full_fx.group(key)
+    cfg, mut, b, s = cases.FULL[key]
+    model = cases.seeded_model(cfg, 0, mut)
+    x = cases.full_input(key, fx)
+    y = Engine(model.to(device), b, s, device)(x.half().to(device)).cpu()
+    assert torch.isfinite(y).all()
+    ref = cases.oracle_model(model.cpu(), x, torch.float32)
+    box = _rel(y[:, :4], ref[:, :4])
+    cls = (y[:, 4:] - ref[:, 4:]).abs().max().item()
+    e_slice, e_sum = cases.compare_full(y, fx)
+    print(f"{key}: box rel {box:.2e} cls abs {cls:.2e} | ref slice {e_slice:.2e} row sums {e_sum:.2e}")
+    assert box <= BOX_TOL and cls <= CLS_TOL, (box, cls)
+    assert e_slice <= BOX_TOL and e_sum <= BOX_TOL, (e_slice, e_sum)
+
+
+@pytest.mark.parametrize("key", list(cases.OPS_FULL))
+def test_full_size_op_parity(key, full_fx, device):
+    """BiCoordCrossAtt at 80x80 / 160x160 and C2PSA at 20x20 / 40x40 (1600 keys), drop-in forward in fp16
+    against the oracle's full tensor and the reference's slices / channel sums."""
+    fx = full_fx.group(key)
+    mod, x = cases.full_op(key, fx)
+    ref = cases.full_op_oracle(key, mod, x)
+    with torch.inference_mode():
+        y = mod.to(device)(x.half().to(device)).float().cpu()
+    assert y.shape == ref.shape and torch.isfinite(y).all()
+    err = _rel(y, ref)
+    e_slice, e_sum = cases.compare_full(y, fx, anchors=False)
+    print(f"{key}: rel {err:.2e} | ref slice {e_slice:.2e} channel sums {e_sum:.2e}")
+    assert err <= OP_TOL and e_slice <= OP_TOL and e_sum <= OP_TOL, (err, e_slice, e_sum)
+
+
 def test_batch_invariance_640(device):
     """Size-independent property at the bench size: an image's detections do not depend on its batch."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)

@@ -71,9 +71,16 @@ def test_coordcrossatt_oup_mismatch_raises():
         mod.emit(Be(), cases.__dict__.get("View", None) or type("V", (), {"n": 1, "h": 4, "w": 4})())
 
 
-def test_cpu_forward_fails_loudly():
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        M.Conv(8, 8, 3)(torch.zeros(1, 8, 4, 4))
+def test_cpu_forward_is_shape_only_never_numeric():
+    """A drop-in on a CPU tensor propagates shapes only (meta output, for the reference's stride probe);
+    reading a value raises.  The package's own whole-model forward refuses CPU input outright."""
+    y = M.Conv(8, 16, 3, 2)(torch.zeros(1, 8, 5, 4))
+    assert y.device.type == "meta" and tuple(y.shape) == (1, 16, 3, 2)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        y.sum().item()
+    det = DetectionModel("yolo11n-fce.yaml").model[-1]
+    maps = det.train()([torch.zeros(1, c, s, s) for c, s in ((64, 8), (128, 4), (256, 2))])
+    assert [tuple(m.shape) for m in maps] == [(1, 144, 8, 8), (1, 144, 4, 4), (1, 144, 2, 2)]
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         DetectionModel("yolo11n-fce.yaml")(torch.zeros(1, 3, 64, 64))
 

@@ -105,3 +105,23 @@ def test_oracle_parser_layer_table(name, tables):
         assert L["i"] == row["i"] and L["f"] == row["f"]
         assert L["type"] == row["type"] or (L["type"] == "Upsample" and row["type"] == "Upsample")
         assert str(L["args"]).replace("'", "") == row["args"].replace("'", ""), (L, row)
+
+
+@pytest.mark.parametrize("key", list(cases.FULL))
+def test_oracle_full_size_matches_reference(key, full_fx):
+    """The oracle at the BASELINE configs' real sizes (m-h8 @1280: C2PSA over 1600 keys, BiCoord at 160x160)
+    against the reference's slices / row sums (golden/full.npz)."""
+    fx = full_fx.group(key)
+    cfg, mut, _, _ = cases.FULL[key]
+    y = cases.oracle_model(cases.seeded_model(cfg, 0, mut), cases.full_input(key, fx), torch.float32)
+    e_slice, e_sum = cases.compare_full(y, fx)
+    assert e_slice < 2e-5 and e_sum < 1e-6, (e_slice, e_sum)
+
+
+@pytest.mark.parametrize("key", list(cases.OPS_FULL))
+def test_oracle_full_size_ops_match_reference(key, full_fx):
+    fx = full_fx.group(key)
+    mod, x = cases.full_op(key, fx)
+    y = cases.full_op_oracle(key, mod, x)
+    e_slice, e_sum = cases.compare_full(y, fx, anchors=False)
+    assert e_slice < 2e-5 and e_sum < 1e-6, (e_slice, e_sum)
