@@ -4,13 +4,14 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-A step = the whole forward (direct launches; --graph 1 for hipGraph replay) over a resident synthetic
-batch (torch.rand(B,3,S,S) fp16, seeded per rank) + the device NMS of that batch.  By default the NMS of
-batch i runs on a side stream under the forward of batch i+1 (engine.Pipeline, double-buffered pred);
---sequential runs them back to back.  Weights are the
-portable seeded weights of the named architecture (no checkpoints offline), broadcast from rank 0
-over RCCL.  Each rank owns its own batch shard (contiguous, reference ContiguousDistributedSampler
-rule); there is no data-path collective, so scaling is weak.  Prints ONE JSON line on rank 0.
+A step = one global batch of B images per GPU through `dist.ShardedPredictor`: each rank's contiguous
+shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
+per rank) runs the whole forward (direct launches; --graph 1 for hipGraph replay) + the device NMS, and
+with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  The
+NMS + gather of batch i run on a side stream under the forward of batch i+1 (engine.Pipeline);
+--sequential runs forward and NMS back to back.  Weights are the portable seeded weights of the named
+architecture (no checkpoints offline), broadcast from rank 0 over RCCL.  Per-GPU work is fixed as N
+grows: scaling is weak.  Prints ONE JSON line on rank 0.
 """
 
 from __future__ import annotations
@@ -31,8 +32,8 @@ sys.path.insert(0, str(ROOT))
 import fce_pkg  # noqa: E402
 
 fce_pkg.load()
-from fce_yolo_amd.dist import broadcast_module  # noqa: E402
-from fce_yolo_amd.engine import NMS, Engine, Pipeline  # noqa: E402
+from fce_yolo_amd.dist import ShardedPredictor, broadcast_module  # noqa: E402
+from fce_yolo_amd.engine import NMS  # noqa: E402
 from fce_yolo_amd.parser import DetectionModel, load_cfg  # noqa: E402
 from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
 
@@ -150,11 +151,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
-    local = local % max(1, torch.cuda.device_count())  # (rehearsals with more ranks than GPUs)
+    backend = os.environ.get("FCE_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        if world > 1 and backend == "nccl":
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): one RCCL rank per GPU")
+        local = local % max(1, ndev)  # gloo rehearsal with more ranks than GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("FCE_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     model = DetectionModel(model_cfg(a.model))
@@ -165,18 +170,20 @@ def main():
         broadcast_module(model, src=0)
 
     B, S = a.batch, a.imgsz
+    # this rank's contiguous shard of a global batch of B * world images (dist.ShardedPredictor)
+    sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")))
+    eng = sp.engine
+    eng.graph = bool(a.graph)
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
-    eng = Engine(model, B, S, dev, graph=bool(a.graph))
     nms = NMS(B, eng.anchors, eng.nc, dev)
-    pipe = Pipeline(eng, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")))
 
     def step():
         if a.no_nms:
             eng(x)
         elif a.sequential:
             nms(eng(x))
-        else:  # forward of this batch overlaps the NMS of the previous one (engine.Pipeline)
-            pipe.submit(x)
+        else:  # forward of this batch overlaps the NMS (+ multi-GPU gather) of the previous one
+            sp.submit(x)
 
     def barrier():
         if world > 1:
@@ -293,7 +300,7 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    eng.close()
+    sp.close()
 
 
 if __name__ == "__main__":

@@ -217,12 +217,20 @@ struct fce_net {
   size_t ws_bytes = 0;
   int anchors = 0, nc = 0;
   int level_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  const void* cap_in = nullptr;
-  float* cap_out = nullptr;
-  hipStream_t cap_stream = nullptr;
-  fce_tensor cap_desc{};
+  // captured forwards, one per (input, pred, stream, input dtype / channels): a double-buffered caller
+  // (engine.Pipeline alternates two pred buffers) replays its graphs instead of recapturing
+  struct Captured {
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    const void* in;
+    float* out;
+    hipStream_t stream;
+    int dtype, c;
+    unsigned long long used;
+  };
+  static constexpr int kMaxGraphs = 4;
+  std::vector<Captured> graphs;
+  unsigned long long graph_clock = 0;
   // multi-stream capture: side streams + one event per op (+ fork), created on first capture
   std::vector<hipStream_t> side;
   std::vector<hipEvent_t> op_ev;
@@ -245,13 +253,13 @@ struct fce_net {
     own = nullptr;
   }
 
-  void drop_graph() {
-    if (exec) (void)hipGraphExecDestroy(exec);
-    if (graph) (void)hipGraphDestroy(graph);
-    exec = nullptr;
-    graph = nullptr;
-    cap_in = nullptr;
-    cap_out = nullptr;
+  static void destroy(Captured& c) {
+    if (c.exec) (void)hipGraphExecDestroy(c.exec);
+    if (c.graph) (void)hipGraphDestroy(c.graph);
+  }
+  void drop_graph() {  // every captured forward (the plan, a buffer or an op variant changed)
+    for (Captured& c : graphs) destroy(c);
+    graphs.clear();
   }
   void release() {
     drop_graph();
@@ -834,10 +842,17 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
       FCE_HIP_CHECK(hipEventRecord(net->join_ev[0], caller));
       FCE_HIP_CHECK(hipStreamWaitEvent(s, net->join_ev[0], 0));
     }
-    const bool same = net->exec && net->cap_in == input->data && net->cap_out == pred && net->cap_stream == s &&
-                      net->cap_desc.dtype == input->dtype && net->cap_desc.c == input->c;
-    if (!same) {
-      net->drop_graph();
+    fce_net::Captured* hit = nullptr;
+    for (fce_net::Captured& c : net->graphs)
+      if (c.in == input->data && c.out == pred && c.stream == s && c.dtype == input->dtype && c.c == input->c)
+        hit = &c;
+    if (!hit) {
+      if (int(net->graphs.size()) >= fce_net::kMaxGraphs) {  // evict the least recently replayed
+        auto lru = std::min_element(net->graphs.begin(), net->graphs.end(),
+                                    [](const fce_net::Captured& a, const fce_net::Captured& b) { return a.used < b.used; });
+        fce_net::destroy(*lru);
+        net->graphs.erase(lru);
+      }
       FCE_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       st = run_all(net, *input, pred, s);
       hipGraph_t g = nullptr;
@@ -847,14 +862,16 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
         return st;
       }
       FCE_HIP_CHECK(e);
-      net->graph = g;
-      FCE_HIP_CHECK(hipGraphInstantiate(&net->exec, g, nullptr, nullptr, 0));
-      net->cap_in = input->data;
-      net->cap_out = pred;
-      net->cap_stream = s;
-      net->cap_desc = *input;
+      hipGraphExec_t x = nullptr;
+      if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        return fail(FCE_ERR_HIP, "fce_net_forward: hipGraphInstantiate failed");
+      }
+      net->graphs.push_back({g, x, input->data, pred, s, input->dtype, input->c, 0});
+      hit = &net->graphs.back();
     }
-    FCE_HIP_CHECK(hipGraphLaunch(net->exec, s));
+    hit->used = ++net->graph_clock;
+    FCE_HIP_CHECK(hipGraphLaunch(hit->exec, s));
     if (s != caller) {
       FCE_HIP_CHECK(hipEventRecord(net->join_ev[1], s));
       FCE_HIP_CHECK(hipStreamWaitEvent(caller, net->join_ev[1], 0));
@@ -947,6 +964,7 @@ int fce_net_set_op_variant(fce_net* net, int i, int code) {
     const int nc = fce_net_op_variants(net, i, cand, 128);
     FCE_CHECK(std::find(cand, cand + nc, code) != cand + nc, "fce_net_set_op_variant: not a candidate of this op");
   }
+  if (op.tile != code) net->drop_graph();  // captured forwards hold the old variant's launches
   op.tile = code;
   return FCE_OK;
 }

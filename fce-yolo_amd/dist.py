@@ -5,8 +5,14 @@
   lowest ranks, and a batch size >= the dataset degenerating to batch size 1.
 * `broadcast_module` sends rank 0's weights to every rank once per model load (RCCL over xGMI on the
   GPU box, gloo on CPU).
-* `gather_detections` collects every rank's post-NMS detections on all ranks (outside the timed loop).
-No collective is on the per-step data path: the bench scales weakly.
+* `gather_detections` collects every rank's post-NMS detections on all ranks (variable sizes, host sync).
+* `ShardedPredictor` is the per-step multi-GPU entry point (`bench.py --gpus N`): rank r runs its
+  contiguous shard of each global batch through Engine + Pipeline, and the packed post-NMS outputs of
+  every rank are all-gathered (one RCCL collective per batch, ~0.3 MB per rank at bs 32) on the NMS side
+  stream, overlapped with the next batch's forward -- the reference's ``gather_object`` of validation
+  results to rank 0 (models/yolo/detect/val.py:222-241), without a host round trip.  Per-image results
+  come back in the unsharded order (`unpack_gathered`).
+Images never cross GPUs; the gather is the only per-step collective and the bench scales weakly.
 """
 
 from __future__ import annotations
@@ -82,3 +88,85 @@ def gather_detections(dets: torch.Tensor, keep: torch.Tensor, counts: torch.Tens
         res_d += [outs[0][r][i, : cnt[i]] for i in range(n)]
         res_k += [outs[1][r][i, : cnt[i]] for i in range(n)]
     return res_d, res_k
+
+
+def shard_sizes(total: int, world: int, batch_size: int) -> list[int]:
+    """Images of every rank under `shard_range`."""
+    return [e - s for s, e in (shard_range(total, world, r, batch_size) for r in range(world))]
+
+
+def unpack_gathered(gathered: torch.Tensor, sizes: list[int], max_det: int):
+    """All ranks' packed NMS outputs (``engine.NMS`` layout, each padded to max(sizes) images, rank order)
+    -> (dets, keep) per image in the unsharded order: rank r's images are global images
+    [sum(sizes[:r]), sum(sizes[:r+1]))."""
+    from .engine import NMS
+
+    bmax = max(sizes)
+    nb = NMS.packed_bytes(bmax, max_det)
+    blocks = gathered.view(len(sizes), nb)
+    dets, keep = [], []
+    for r, n in enumerate(sizes):
+        k, d, c = NMS.unpack(blocks[r], bmax, max_det)
+        cnt = c[:n].tolist()
+        dets += [d[i, : cnt[i]] for i in range(n)]
+        keep += [k[i, : cnt[i]] for i in range(n)]
+    return dets, keep
+
+
+class ShardedPredictor:
+    """Batch-sharded detection inference, one process per GPU.
+
+    A global batch of `total` images is split by `shard_range` (reference ContiguousDistributedSampler,
+    data/build.py:115-215; l256 on 8 GPUs = 8 x 32).  `submit(x)` takes this rank's shard, runs forward
+    + NMS through `engine.Pipeline`, and all-gathers the packed NMS outputs of every rank on the NMS side
+    stream (``dist.all_gather_into_tensor``; RCCL over xGMI on the GPU box), so the gather of batch i
+    overlaps the forward of batch i+1.  `results(k)` unpacks slot k in the unsharded image order."""
+
+    def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, depth: int = 2, **nms_kw):
+        from .engine import NMS, Engine, Pipeline
+
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        bs = batch_size or -(-total // self.world)
+        self.sizes = shard_sizes(total, self.world, bs)
+        self.start, self.end = shard_range(total, self.world, self.rank, bs)
+        self.batch = self.end - self.start
+        if self.batch <= 0:
+            raise ValueError(f"rank {self.rank}: empty shard of a {total}-image batch over {self.world} ranks")
+        self.bmax = max(self.sizes)
+        self.engine = Engine(model, self.batch, imgsz, device)
+        self.max_det = nms_kw.get("max_det", 300)
+        nb = NMS.packed_bytes(self.bmax, self.max_det)
+        # each rank's packed outputs padded to bmax images, so every rank contributes the same bytes
+        self.send = [torch.zeros(nb if self.batch < self.bmax else 0, dtype=torch.uint8, device=device)
+                     for _ in range(depth)]
+        self.gathered = [torch.zeros(self.world * nb if self.world > 1 else 0, dtype=torch.uint8, device=device)
+                         for _ in range(depth)]
+        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.world > 1 else None, **nms_kw)
+
+    def _gather(self, k: int):
+        from .engine import NMS
+
+        nms = self.pipe.nms[k]
+        send = nms.buf
+        if self.batch < self.bmax:  # a remainder shard: re-pack into the bmax layout every rank sends
+            send = self.send[k]
+            keep, dets, counts = NMS.unpack(send, self.bmax, self.max_det)
+            keep[: self.batch].copy_(nms.keep)
+            dets[: self.batch].copy_(nms.dets)
+            counts[: self.batch].copy_(nms.counts)
+        dist.all_gather_into_tensor(self.gathered[k], send)
+
+    def submit(self, x: torch.Tensor) -> int:
+        if x.shape[0] != self.batch:
+            raise ValueError(f"rank {self.rank}: shard of {self.batch} images expected, got {x.shape[0]}")
+        return self.pipe.submit(x)
+
+    def results(self, k: int):
+        """(dets, keep) per image of the whole global batch, in the unsharded order."""
+        self.pipe.nms_done[k].synchronize()
+        g = self.gathered[k] if self.world > 1 else self.pipe.nms[k].buf
+        return unpack_gathered(g, self.sizes, self.max_det)
+
+    def close(self):
+        self.engine.close()

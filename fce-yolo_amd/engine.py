@@ -114,10 +114,23 @@ class NMS:
         self.conf, self.iou, self.max_det, self.max_nms, self.max_wh = conf, iou, max_det, max_nms, max_wh
         nb = N.lib().fce_nms_workspace_bytes(batch, anchors, max_nms)
         self.ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
-        self.dets = torch.zeros((batch, max_det, 6), dtype=torch.float32, device=device)
-        self.keep = torch.zeros((batch, max_det), dtype=torch.int64, device=device)
-        self.counts = torch.zeros((batch,), dtype=torch.int32, device=device)
+        # outputs packed in one buffer (keep | dets | counts), so a multi-GPU gather is one collective
+        self.buf = torch.zeros(self.packed_bytes(batch, max_det), dtype=torch.uint8, device=device)
+        self.keep, self.dets, self.counts = self.unpack(self.buf, batch, max_det)
         self.device = device
+
+    @staticmethod
+    def packed_bytes(batch: int, max_det: int) -> int:
+        return batch * max_det * (8 + 24) + (batch * 4 + 15) // 16 * 16  # 16-byte multiple: blocks stay aligned
+
+    @staticmethod
+    def unpack(buf: torch.Tensor, batch: int, max_det: int):
+        """(keep (b,max_det) i64, dets (b,max_det,6) f32, counts (b,) i32) views of a packed output buffer."""
+        k, d = batch * max_det * 8, batch * max_det * 24
+        keep = buf[:k].view(torch.int64).view(batch, max_det)
+        dets = buf[k:k + d].view(torch.float32).view(batch, max_det, 6)
+        counts = buf[k + d:k + d + batch * 4].view(torch.int32)
+        return keep, dets, counts
 
     def __call__(self, pred: torch.Tensor):
         assert pred.is_contiguous() and pred.dtype == torch.float32 and tuple(pred.shape) == (
@@ -157,8 +170,10 @@ class Pipeline:
     `wait(slot)` (or a device sync) has passed.
     """
 
-    def __init__(self, engine: Engine, depth: int = 2, **nms_kw):
-        self.eng, self.depth = engine, depth
+    def __init__(self, engine: Engine, depth: int = 2, post=None, **nms_kw):
+        """`post(k)`, if given, runs on the side stream right after slot k's NMS (e.g. the multi-GPU gather
+        of its outputs, dist.ShardedPredictor); the slot is reused only after it too has finished."""
+        self.eng, self.depth, self.post = engine, depth, post
         dev = engine.device
         self.preds = [torch.empty_like(engine.pred) for _ in range(depth)]
         self.nms = [NMS(engine.batch, engine.anchors, engine.nc, dev, **nms_kw) for _ in range(depth)]
@@ -179,6 +194,8 @@ class Pipeline:
         self.side.wait_event(self.fwd_done[k])
         with torch.cuda.stream(self.side):
             self.nms[k](self.preds[k])
+            if self.post is not None:
+                self.post(k)
             self.nms_done[k].record(self.side)
         self.used[k] = True
         return k

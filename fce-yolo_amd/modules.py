@@ -44,9 +44,19 @@ def autopad(k, p=None, d=1):
 
 
 # ============================================================================ native weight cache
+def _tkey(t: torch.Tensor):
+    """Identity of a weight tensor's contents: storage, version counter, dtype.  Inference tensors (e.g.
+    buffers of a module moved inside ``torch.inference_mode``) have no version counter; they are keyed by
+    storage and dtype only."""
+    try:
+        return t.data_ptr(), t._version, t.dtype
+    except RuntimeError:
+        return t.data_ptr(), -1, t.dtype
+
+
 def _state_key(mod: nn.Module, device):
     ts = list(mod.parameters()) + list(mod.buffers())
-    return (str(device),) + tuple((t.data_ptr(), t._version, t.dtype) for t in ts)
+    return (str(device),) + tuple(_tkey(t) for t in ts)
 
 
 def _cached(mod: nn.Module, device, build, slot: str = "_fce_native"):
@@ -125,7 +135,7 @@ def conv_native(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, act: bool, device) -
 
     # cached on the conv module; the key covers the conv's and the BN's tensors
     ts = list(conv.parameters()) + list(conv.buffers()) + (list(bn.parameters()) + list(bn.buffers()) if bn else [])
-    key = (str(device), act) + tuple((t.data_ptr(), t._version, t.dtype) for t in ts)
+    key = (str(device), act) + tuple(_tkey(t) for t in ts)
     c = conv.__dict__.get("_fce_conv")
     if c is None or c[0] != key:
         c = (key, build())

@@ -14,7 +14,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import fce_pkg  # noqa: E402  (spawned workers import this module fresh)
 
 fce_pkg.load()
-from fce_yolo_amd.dist import broadcast_module, gather_detections, shard_range  # noqa: E402
+from fce_yolo_amd.dist import broadcast_module, gather_detections, shard_range, shard_sizes, unpack_gathered  # noqa: E402
+from fce_yolo_amd.engine import NMS  # noqa: E402
 
 
 def _ref_rule(total, world, rank, bs):
@@ -80,3 +81,51 @@ def test_broadcast_and_gather_gloo_world2():
     assert d0 == d1  # rank 1 now holds rank 0's weights
     assert s0 == s1 == [(1, 6), (2, 6), (3, 6), (1, 6), (2, 6)]
     assert k0 == k1 == [[0], [5, 6], [10, 11, 12], [100], [105, 106]]
+
+
+def _packed_shard(rank, n, bmax, max_det, first):
+    """This rank's NMS outputs in the packed engine.NMS layout (padded to bmax images); image i of the
+    global batch keeps 1 + i % 4 boxes whose anchor indices encode (image, j)."""
+    buf = torch.zeros(NMS.packed_bytes(bmax, max_det), dtype=torch.uint8)
+    keep, dets, counts = NMS.unpack(buf, bmax, max_det)
+    for i in range(n):
+        g = first + i
+        c = 1 + g % 4
+        counts[i] = c
+        keep[i, :c] = torch.arange(c) + 1000 * g
+        dets[i, :c] = float(g)
+    return buf
+
+
+def _sharded_worker(rank, world, port, q, total, bs, max_det):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sizes = shard_sizes(total, world, bs)
+        s, e = shard_range(total, world, rank, bs)
+        buf = _packed_shard(rank, e - s, max(sizes), max_det, s)
+        out = torch.empty(world * buf.numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, buf)  # the ShardedPredictor collective
+        dets, keep = unpack_gathered(out, sizes, max_det)
+        q.put((rank, [k.tolist() for k in keep], [float(d[0, 0]) if len(d) else None for d in dets]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,bs", [(7, 2), (5, 3), (8, 4)])
+def test_sharded_gather_restores_unsharded_order_gloo_world2(total, bs):
+    """Uneven (remainder-rule) shards: the gathered per-image results come back in the global order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q, total, bs, 6)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [[1000 * g + j for j in range(1 + g % 4)] for g in range(total)]
+    for _, keep, first in res:
+        assert keep == want
+        assert first == [float(g) for g in range(total)]
