@@ -13,6 +13,9 @@
 // Everything is deterministic (fixed reduction orders, no atomics).
 #include "common.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace fce {
 
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
@@ -54,9 +57,8 @@ size_t coord_ws_bytes(const fce_coord_desc& d, int n, int h, int w) {
 }
 
 // ---------------------------------------------------------------------------- 1. pooling
-__global__ __launch_bounds__(256) void pool_rows_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xh) {
+__device__ __forceinline__ void pool_rows(const _Float16* x, int xcs, int H, int W, int C, float* xh, int y, int n) {
   __shared__ float red[256 * 8];
-  const int n = blockIdx.y, y = blockIdx.x;
   const int CG = C / 8;
   const int XT = 256 / CG;
   const int t = threadIdx.x;
@@ -81,38 +83,69 @@ __global__ __launch_bounds__(256) void pool_rows_kernel(const _Float16* x, int x
   }
 }
 
-__global__ __launch_bounds__(256) void pool_cols_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xw) {
-  const int n = blockIdx.y;
+// column means: a block owns XW = 256 / (CG * RG) columns; thread (cg, column, row group) sums its RG-th
+// share of the rows (contiguous row ranges, 8 loads in flight), the RG partials are added in row-group
+// order through LDS (fixed order: deterministic)
+__device__ __forceinline__ int pool_col_groups(int C, int H) {
   const int CG = C / 8;
-  const int XW = 256 / CG;
+  int RG = 1;
+  while (RG < 8 && CG * RG * 2 <= 256 && H >= 16 * RG) RG *= 2;
+  return RG;
+}
+
+__device__ __forceinline__ void pool_cols(const _Float16* x, int xcs, int H, int W, int C, float* xw, int bx, int n) {
+  __shared__ float part[256 * 8];
+  const int CG = C / 8;
+  const int RG = pool_col_groups(C, H);
+  const int XW = 256 / (CG * RG);
   const int t = threadIdx.x;
-  const int cg = t % CG, xi = t / CG;
-  const int xx = blockIdx.x * XW + xi;
-  if (xi >= XW || xx >= W) return;
+  const int cg = t % CG, xi = (t / CG) % XW, rg = t / (CG * XW);
+  const int xx = bx * XW + xi;
+  const bool live = rg < RG && xx < W;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const _Float16* p = x + nhwc_off(n, 0, xx, H, W, xcs) + cg * 8;
-  const int64_t rs = int64_t(W) * xcs;
-  // 8 rows in flight per step (the walk down a column is latency-bound otherwise); rows are still
-  // added in order, so the sum is the sequential one
-  int y = 0;
-  for (; y + 7 < H; y += 8) {
-    h8 v[8];
+  if (live) {
+    const int rows = (H + RG - 1) / RG, y0 = rg * rows, y1 = min(H, y0 + rows);
+    const _Float16* p = x + nhwc_off(n, 0, xx, H, W, xcs) + cg * 8;
+    const int64_t rs = int64_t(W) * xcs;
+    int y = y0;
+    for (; y + 7 < y1; y += 8) {
+      h8 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const h8*>(p + (y + k) * rs);
+      for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const h8*>(p + (y + k) * rs);
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < 8; ++k)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += (float)v[k][j];
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[k][j];
+    }
+    for (; y < y1; ++y) {
+      const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+    }
   }
-  for (; y < H; ++y) {
-    const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+  for (int j = 0; j < 8; ++j) part[t * 8 + j] = acc[j];
+  __syncthreads();
+  if (rg == 0 && live) {
+    const float inv = 1.0f / (float)H;
+    float* o = xw + (int64_t(n) * W + xx) * C + cg * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sum = part[t * 8 + j];
+      for (int r = 1; r < RG; ++r) sum += part[(t + r * CG * XW) * 8 + j];
+      o[j] = sum * inv;
+    }
   }
-  const float inv = 1.0f / (float)H;
-  float* o = xw + (int64_t(n) * W + xx) * C + cg * 8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = acc[j] * inv;
+}
+
+// both poolings in one launch (grid (H + column strips, N)): blocks [0, H) take a row each, the rest a
+// strip of XW columns; the two halves read disjoint work and run side by side
+__global__ __launch_bounds__(256) void pool_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xh,
+                                                   float* xw) {
+  if (int(blockIdx.x) < H)
+    pool_rows(x, xcs, H, W, C, xh, blockIdx.x, blockIdx.y);
+  else
+    pool_cols(x, xcs, H, W, C, xw, blockIdx.x - H, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------- 2. projections
@@ -388,6 +421,216 @@ __global__ __launch_bounds__(256) void coord_attend_groups_kernel(AttArgs a, int
   for (int e = threadIdx.x; e < nq * mid; e += blockDim.x) dst[e] = ys[e];
 }
 
+// ---------------------------------------------------------------------------- 2+3 fused (small problems)
+// BiCoordCrossAtt's whole per-image middle in one workgroup per (image, branch): the branch's q / k / v
+// projections of the pooled vectors (staged in LDS), the axial multi-head attention and the output
+// projection to the gate logits -- one launch instead of projection + attention + projection, for the
+// n / s scales where a branch is ~0.5-2 M MACs.  Branch 0 (h): q <- x_h, k, v <- x_w; branch 1 (w):
+// q <- x_w, k, v <- x_h (fce_block.py:235-284).
+struct CoreArgs {
+  const float* xh;  // [N][H][C]
+  const float* xw;  // [N][W][C]
+  const float* wq[2];
+  const float* bq[2];
+  const float* wk[2];
+  const float* bk[2];
+  const float* wv[2];
+  const float* bv[2];
+  const float* wo[2];  // [mid][oup]
+  const float* bo[2];
+  float* g[2];         // [N][L][oup] gate logits
+  int H, W, C, mid, heads, oup;
+  float scale;
+  unsigned long long* tm;  // diagnostics (FCE_COORD_TIMING): per-workgroup phase clocks, else null
+};
+
+static constexpr int CORE_THREADS = 1024;
+
+// LDS floats of the fused middle: pooled rows of both axes (odd stride), the three projection weights
+// and the output projection, q / k / v / attention outputs
+static size_t core_lds_floats(int H, int W, int C, int mid, int oup) {
+  const int L = H > W ? H : W;
+  return size_t(2) * L * (C + 4) + size_t(3) * C * mid + size_t(mid) * oup + size_t(4) * L * (mid + 4) + 4;
+}
+
+template <int DH>
+__global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = blockIdx.x, br = blockIdx.y;
+  // row strides: lc = C + 4 floats (16-byte rows; a wave's 16 positions land on distinct bank quads),
+  // lm = mid + 4
+  const int C = a.C, mid = a.mid, oup = a.oup, lc = C + 4, lm = mid + 4;
+  const int Lq = br == 0 ? a.H : a.W, Lk = br == 0 ? a.W : a.H;
+  const float* gq = (br == 0 ? a.xh + int64_t(n) * a.H * C : a.xw + int64_t(n) * a.W * C);
+  const float* gk = (br == 0 ? a.xw + int64_t(n) * a.W * C : a.xh + int64_t(n) * a.H * C);
+  const int L = a.H > a.W ? a.H : a.W;
+  float* wq = sm;                // [C][mid]
+  float* wk = wq + C * mid;      // [C][mid]
+  float* wv = wk + C * mid;      // [C][mid]
+  float* wo = wv + C * mid;      // [mid][oup]
+  float* q = wo + mid * oup;     // [Lq][lm]
+  float* k = q + L * lm;         // [Lk][lm]
+  float* v = k + L * lm;         // [Lk][lm]
+  float* ys = v + L * lm;        // [Lq][lm]
+  float* sq = ys + L * lm;       // [Lq][lc]
+  float* skv = sq + L * lc;      // [Lk][lc]
+  unsigned long long t0 = a.tm ? __builtin_amdgcn_s_memtime() : 0;
+  {
+    // all staging (weights, output weights, both pooled axes) as one flat space of 16-byte pieces, 8 loads
+    // per thread in flight before their LDS stores (one memory round trip instead of six)
+    const int C4 = C / 4, nw = C * mid / 4, no4 = mid * oup / 4, nq4 = Lq * C4, nk4 = Lk * C4;
+    const int total = 3 * nw + no4 + nq4 + nk4;
+    float* dummy = skv + L * lc;
+    for (int e0 = 0; e0 < total; e0 += 8 * CORE_THREADS) {
+      f4 val[8];
+      float* dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        int e = e0 + int(threadIdx.x) + u * CORE_THREADS;
+        const bool ok = e < total;
+        e = ok ? e : total - 1;
+        const float* sp;
+        float* dp;
+        if (e < 3 * nw) {
+          const int m = e / nw, r = 4 * (e - m * nw);
+          sp = (m == 0 ? a.wq[br] : m == 1 ? a.wk[br] : a.wv[br]) + r;
+          dp = wq + m * C * mid + r;
+        } else if ((e -= 3 * nw) < no4) {
+          sp = a.wo[br] + 4 * e;
+          dp = wo + 4 * e;
+        } else if ((e -= no4) < nq4) {
+          const int p = e / C4, c = (e - p * C4) * 4;
+          sp = gq + p * C + c;
+          dp = sq + p * lc + c;
+        } else {
+          e -= nq4;
+          const int p = e / C4, c = (e - p * C4) * 4;
+          sp = gk + p * C + c;
+          dp = skv + p * lc + c;
+        }
+        val[u] = *reinterpret_cast<const f4*>(sp);
+        dst[u] = ok ? dp : dummy;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(dst[u]) = val[u];
+    }
+  }
+  __syncthreads();
+  unsigned long long t1 = a.tm ? __builtin_amdgcn_s_memtime() : 0;
+  // projections, task = (matrix, position, 4 consecutive outputs): one broadcast source read and one
+  // 16-byte weight read per 4 FMAs
+  const int mq = mid / 4, tq = Lq * mq, tk = Lk * mq;
+  for (int e = threadIdx.x; e < tq + 2 * tk; e += CORE_THREADS) {
+    int t = e, mat = 0;
+    if (t >= tq) {
+      t -= tq;
+      mat = 1 + (t >= tk);
+      if (t >= tk) t -= tk;
+    }
+    const int p = t / mq, m4 = (t - p * mq) * 4;
+    const float* src = (mat == 0 ? sq : skv) + p * lc;
+    const float* w = (mat == 0 ? wq : mat == 1 ? wk : wv) + m4;
+    const float* b = mat == 0 ? a.bq[br] : mat == 1 ? a.bk[br] : a.bv[br];
+    f4 acc0 = b ? *reinterpret_cast<const f4*>(b + m4) : f4{0.f, 0.f, 0.f, 0.f};
+    f4 acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = acc1, acc3 = acc1;
+#pragma unroll 4
+    for (int c = 0; c < C; c += 4) {  // C % 8 == 0
+      const f4 sv = *reinterpret_cast<const f4*>(src + c);
+      const f4 w0 = *reinterpret_cast<const f4*>(w + c * mid), w1 = *reinterpret_cast<const f4*>(w + (c + 1) * mid);
+      const f4 w2 = *reinterpret_cast<const f4*>(w + (c + 2) * mid), w3 = *reinterpret_cast<const f4*>(w + (c + 3) * mid);
+      acc0 += sv[0] * w0;
+      acc1 += sv[1] * w1;
+      acc2 += sv[2] * w2;
+      acc3 += sv[3] * w3;
+    }
+    *reinterpret_cast<f4*>((mat == 0 ? q : mat == 1 ? k : v) + p * lm + m4) = (acc0 + acc1) + (acc2 + acc3);
+  }
+  __syncthreads();
+  unsigned long long t2 = a.tm ? __builtin_amdgcn_s_memtime() : 0;
+  // attention: G lanes per (query, head) split the keys (lane g takes keys g, g + G, ..); two passes
+  // (row max, then exp-sum and P.V) so each key costs one exp, the G partial states merged by xor-shuffles
+  const int pairs = Lq * a.heads;
+  int G = 1;
+  while (G < 16 && pairs * G * 2 <= CORE_THREADS) G *= 2;
+  for (int e0 = 0; e0 < pairs * G; e0 += CORE_THREADS) {
+    const int e = e0 + int(threadIdx.x);
+    const bool live = e < pairs * G;
+    const int pr = live ? e / G : 0, gl = e % G;
+    const int i = pr / a.heads, hd = pr - i * a.heads;
+    float qq[DH], acc[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) {
+      qq[d] = q[i * lm + hd * DH + d] * a.scale;
+      acc[d] = 0.f;
+    }
+    float m = -INFINITY;
+#pragma unroll 4
+    for (int j = gl; j < Lk; j += G) {
+      const float* kj = k + j * lm + hd * DH;
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
+      m = fmaxf(m, sc);
+    }
+    for (int off = 1; off < G; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+    float l = 0.f;
+#pragma unroll 4
+    for (int j = gl; j < Lk; j += G) {
+      const float* kj = k + j * lm + hd * DH;
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
+      const float pj = __expf(sc - m);
+      l += pj;
+      const float* vj = v + j * lm + hd * DH;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[d] += pj * vj[d];
+    }
+    for (int off = 1; off < G; off <<= 1) {
+      l += __shfl_xor(l, off);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[d] += __shfl_xor(acc[d], off);
+    }
+    if (live && gl == 0) {
+      const float inv = 1.0f / l;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) ys[i * lm + hd * DH + d] = acc[d] * inv;
+    }
+  }
+  __syncthreads();
+  unsigned long long t3 = a.tm ? __builtin_amdgcn_s_memtime() : 0;
+  // output projection to the gate logits, task = (position, 4 consecutive outputs), 16-byte stores
+  float* g = a.g[br] + int64_t(n) * Lq * oup;
+  const float* bo = a.bo[br];
+  const int o4n = oup / 4;
+  for (int e = threadIdx.x; e < Lq * o4n; e += CORE_THREADS) {
+    const int i = e / o4n, o4 = (e - i * o4n) * 4;
+    const float* y = ys + i * lm;
+    f4 acc0 = bo ? *reinterpret_cast<const f4*>(bo + o4) : f4{0.f, 0.f, 0.f, 0.f};
+    f4 acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = acc1, acc3 = acc1;
+    for (int m2 = 0; m2 < mid; m2 += 4) {  // mid % 4 == 0
+      const f4 yv = *reinterpret_cast<const f4*>(y + m2);
+      acc0 += yv[0] * *reinterpret_cast<const f4*>(wo + m2 * oup + o4);
+      acc1 += yv[1] * *reinterpret_cast<const f4*>(wo + (m2 + 1) * oup + o4);
+      acc2 += yv[2] * *reinterpret_cast<const f4*>(wo + (m2 + 2) * oup + o4);
+      acc3 += yv[3] * *reinterpret_cast<const f4*>(wo + (m2 + 3) * oup + o4);
+    }
+    *reinterpret_cast<f4*>(g + i * oup + o4) = (acc0 + acc1) + (acc2 + acc3);
+  }
+  if (a.tm) {
+    __syncthreads();
+    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* o = a.tm + (blockIdx.y * gridDim.x + blockIdx.x) * 5;
+      o[0] = t0;
+      o[1] = t1 - t0;
+      o[2] = t2 - t1;
+      o[3] = t3 - t2;
+      o[4] = t4 - t3;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
@@ -508,6 +751,78 @@ static int launch_attend(AttJob* jobs, int nj, int N, const fce_coord_desc& d, h
   return launch_status("coord_attend_kernel");
 }
 
+// the fused middle for problems of <= ~2 M MACs per (image, branch) whose staging fits in LDS
+static constexpr size_t kCoreMaxMacs = size_t(2) << 20;
+static bool use_core(const fce_coord_desc& d, int H, int W) {
+  const size_t L = size_t(H > W ? H : W);
+  const int dh = d.mid / d.heads;
+  return (dh == 1 || dh == 2 || dh == 4 || dh == 8 || dh == 16) && d.mid % 4 == 0 && d.oup % 4 == 0 &&
+         3 * L * d.mid * d.inp <= kCoreMaxMacs && core_lds_floats(H, W, d.inp, d.mid, d.oup) * sizeof(float) <= 160 * 1024;
+}
+
+static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, int W, hipStream_t s) {
+  CoreArgs a;
+  a.xh = w.xh;
+  a.xw = w.xw;
+  for (int br = 0; br < 2; ++br) {
+    a.wq[br] = d.w[3 * br + 0];
+    a.bq[br] = d.b[3 * br + 0];
+    a.wk[br] = d.w[3 * br + 1];
+    a.bk[br] = d.b[3 * br + 1];
+    a.wv[br] = d.w[3 * br + 2];
+    a.bv[br] = d.b[3 * br + 2];
+    a.wo[br] = d.w[6 + br];
+    a.bo[br] = d.b[6 + br];
+  }
+  a.g[0] = w.g1;
+  a.g[1] = w.g2;
+  a.H = H;
+  a.W = W;
+  a.C = d.inp;
+  a.mid = d.mid;
+  a.heads = d.heads;
+  a.oup = d.oup;
+  a.scale = d.scale;
+  a.tm = nullptr;
+  static unsigned long long* tm_buf = nullptr;
+  const char* tenv = getenv("FCE_COORD_TIMING");
+  if (tenv && atoi(tenv)) {
+    if (!tm_buf) FCE_HIP_CHECK(hipMalloc(&tm_buf, size_t(2) * 4096 * 5 * 8));
+    a.tm = N <= 4096 ? tm_buf : nullptr;
+  }
+  const size_t shm = core_lds_floats(H, W, d.inp, d.mid, d.oup) * sizeof(float);
+  switch (d.mid / d.heads) {
+#define CORE(DH)                                                                                              \
+  case DH: {                                                                                                  \
+    static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&coord_core_kernel<DH>),     \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,               \
+                                                    160 * 1024) == hipSuccess;                                \
+    if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord core: cannot opt in to >64 KiB LDS");     \
+    FCE_LAUNCH(coord_core_kernel<DH>, dim3(N, 2), dim3(CORE_THREADS), shm, s, a);                                      \
+    break;                                                                                                    \
+  }
+    CORE(1) CORE(2) CORE(4) CORE(8) CORE(16)
+#undef CORE
+    default:
+      return fail(FCE_ERR_UNSUPPORTED, "coord core: head dim");
+  }
+  int st = launch_status("coord_core_kernel");
+  if (!st && a.tm) {  // diagnostics: print the phase clocks of this launch
+    std::vector<unsigned long long> h(size_t(2) * N * 5);
+    FCE_HIP_CHECK(hipStreamSynchronize(s));
+    FCE_HIP_CHECK(hipMemcpy(h.data(), a.tm, h.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long mn = ~0ull, mx = 0, ph[4] = {0, 0, 0, 0};
+    for (int b = 0; b < 2 * N; ++b) {
+      mn = std::min(mn, h[b * 5]);
+      mx = std::max(mx, h[b * 5]);
+      for (int k = 0; k < 4; ++k) ph[k] += h[b * 5 + 1 + k];
+    }
+    fprintf(stderr, "coord_core N%d H%d W%d: start spread %llu, mean phase clocks stage %llu proj %llu attend %llu out %llu\n",
+            N, H, W, mx - mn, ph[0] / (2 * N), ph[1] / (2 * N), ph[2] / (2 * N), ph[3] / (2 * N));
+  }
+  return st;
+}
+
 static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, const fce_tensor& y, void* ws,
                         size_t ws_bytes, hipStream_t s) {
   FCE_CHECK(x.layout == FCE_NHWC && y.layout == FCE_NHWC && x.dtype == FCE_F16 && y.dtype == FCE_F16,
@@ -526,12 +841,16 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   ws_layout(d, N, H, W, &w, static_cast<float*>(ws));
   const _Float16* xp = static_cast<const _Float16*>(x.data) + x.coff;
   const int C = d.inp, mid = d.mid;
-  FCE_LAUNCH(pool_rows_kernel, dim3(H, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh);
-  const int XW = 256 / (C / 8);
-  FCE_LAUNCH(pool_cols_kernel, dim3((W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xw);
+  int RG = 1;  // pool_col_groups on the host
+  while (RG < 8 && (C / 8) * RG * 2 <= 256 && H >= 16 * RG) RG *= 2;
+  const int XW = 256 / ((C / 8) * RG);
+  FCE_LAUNCH(pool_kernel, dim3(H + (W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.xw);
   int st = launch_status("coord pooling");
   if (st) return st;
-  if (kind == 0) {  // BiCoordCrossAtt
+  const char* nc = getenv("FCE_COORD_NO_CORE");  // diagnostics: force the split projection / attention path
+  if (kind == 0 && !(nc && atoi(nc)) && use_core(d, H, W)) {
+    if ((st = launch_core(d, w, N, H, W, s))) return st;
+  } else if (kind == 0) {  // BiCoordCrossAtt
     ProjJob pj[6] = {
         {w.xh, d.w[0], d.b[0], w.buf[0], H, C, mid, ACT_NONE_},  // q_h  <- x_h
         {w.xw, d.w[1], d.b[1], w.buf[1], W, C, mid, ACT_NONE_},  // k_h  <- x_w

@@ -44,3 +44,18 @@ t = nms.dets[:4, :2, :].reshape(4, 12)[:, :8].cpu().tolist()
 print("segment clocks [select, colmask, resolve, window, tiles, extensions, ext-tests, tail] (s_memtime):")
 for r in t:
     print("  ", [int(v) for v in r])
+# greedy depth: sorted rank (score desc, anchor asc) of the last kept candidate per image
+os.environ["FCE_NMS_STOP"] = "0"
+nms(pred)
+torch.cuda.synchronize()
+sc, cl = pred[:, 4:].max(1)
+depth = []
+for b in range(min(B, 8)):
+    s = sc[b].double().cpu()
+    cand = torch.nonzero(s > 0.25).flatten()
+    order = sorted(cand.tolist(), key=lambda a: (-float(s[a]), a))
+    rank = {a: i for i, a in enumerate(order)}
+    k = nms.keep[b, : int(nms.counts[b])].cpu().tolist()
+    same = sum(1 for i in range(len(order) - 1) if float(s[order[i]]) == float(s[order[i + 1]]))
+    depth.append((max(rank[a] for a in k) + 1 if k else 0, len(order), same))
+print("greedy depth (last kept rank + 1, candidates, equal-score neighbours):", depth)

@@ -35,7 +35,7 @@ def family(name):
         return "conv1x1_detect_box" if out == 4 else "conv1x1_detect_cls" if out == 5 else "conv1x1_mfma"
     for key, fam in (("conv3x3_tile", "conv3x3_mfma"), ("conv3x3_ring", "conv3x3_mfma"), ("stem", "conv_stem"), ("psa_attention", "psa_attention"),
                      ("dwconv", "dwconv3x3"), ("maxpool", "maxpool_chain"), ("weighted_add", "bifpn_weighted_add"),
-                     ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"),
+                     ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"), ("pool_kernel", "bicoordcrossatt"),
                      ("coord_", "bicoordcrossatt"), ("gate_apply", "bicoordcrossatt"), ("nms", "nms"),
                      ("detect_decode", "detect_decode")):
         if key in name:

@@ -68,6 +68,22 @@ def test_op_parity(name, ops_fx, device):
     assert err <= OP_TOL, err
 
 
+@pytest.mark.parametrize("name", ["bicoord_n", "bicoord_l_dh16", "bicoord_h8", "bicoord_oup", "bicoord_dh2"])
+def test_bicoord_fused_core_and_split_paths(name, ops_fx, device, monkeypatch):
+    """The one-launch middle (coord_core_kernel) and the split projection / attention / projection path
+    both against the reference fixture, and against each other."""
+    fx = ops_fx.group(name)
+    mod = cases.build_op(name, fx).to(device)
+    x = cases.op_inputs(fx)[0].to(device).half()
+    ref = torch.from_numpy(fx["out"])
+    with torch.no_grad():
+        yc = mod(x).float()
+        monkeypatch.setenv("FCE_COORD_NO_CORE", "1")
+        ys = mod(x).float()
+    assert _rel(yc, ref) <= OP_TOL and _rel(ys, ref) <= OP_TOL
+    assert _rel(yc, ys) <= 2e-3
+
+
 def test_op_fp32_dropin_keeps_dtype(ops_fx, device):
     fx = ops_fx.group("conv_k3s1")
     mod = cases.build_op("conv_k3s1", fx).to(device)
