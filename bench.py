@@ -181,7 +181,7 @@ def main():
         if a.no_nms:
             eng(x)
         elif a.sequential:
-            nms(eng(x))
+            nms(eng(x), eng.best)
         else:  # forward of this batch overlaps the NMS (+ multi-GPU gather) of the previous one
             sp.submit(x)
 

@@ -62,6 +62,7 @@ class DetectEpi(C.Structure):
         ("reg_max", C.c_int),
         ("part", C.c_int),
         ("stride", C.c_float),
+        ("best", C.c_void_p),
     ]
 
 
@@ -108,6 +109,7 @@ _SIGS = {
     "fce_detect_decode": (_I, [_PT, _PT, _I, _P, _I, _P, _P]),
     "fce_nms_workspace_bytes": (_SZ, [_I, _I, _I]),
     "fce_nms": (_I, [_P, _I, _I, _I, C.c_float, C.c_float, _I, _I, C.c_float, _P, _SZ, _P, _P, _P, _P]),
+    "fce_nms_best": (_I, [_P, _P, _I, _I, _I, C.c_float, C.c_float, _I, _I, C.c_float, _P, _SZ, _P, _P, _P, _P]),
     "fce_copy": (_I, [_PT, _PT, _P]),
     "fce_net_create": (_P, []),
     "fce_net_destroy": (None, [_P]),
@@ -123,6 +125,7 @@ _SIGS = {
     "fce_net_arena_bytes": (_SZ, [_P]),
     "fce_net_num_anchors": (_I, [_P]),
     "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),
+    "fce_net_forward_best": (_I, [_P, _PT, _P, _P, _I, _P]),
     "fce_net_profile": (_I, [_P, _PT, _P, _P, _P, _I, _P]),
     "fce_net_num_ops": (_I, [_P]),
     "fce_net_op_variant": (_I, [_P, _I]),

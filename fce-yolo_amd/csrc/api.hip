@@ -38,7 +38,8 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
 int detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
                   float* out, hipStream_t s);
 size_t nms_ws_bytes(int n, int A, int max_nms);
-int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
+int nms(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou, int max_det,
+        int max_nms, float max_wh,
         void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
 
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
@@ -150,7 +151,15 @@ size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms) { return nms_ws_
 int fce_nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
             void* ws, size_t wsb, float* dets, int64_t* keep, int32_t* counts, void* stream) {
   FCE_CHECK(pred && dets && keep && counts, "fce_nms: null argument");
-  FCE_GUARD(return nms(pred, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts, S(stream));)
+  FCE_GUARD(return nms(pred, nullptr, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts,
+                       S(stream));)
+}
+int fce_nms_best(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou,
+                 int max_det, int max_nms, float max_wh, void* ws, size_t wsb, float* dets, int64_t* keep,
+                 int32_t* counts, void* stream) {
+  FCE_CHECK(pred && best && dets && keep && counts, "fce_nms_best: null argument");
+  FCE_GUARD(return nms(pred, best, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts,
+                       S(stream));)
 }
 int fce_letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad_value, void* stream) {
   FCE_GUARD(return letterbox(imgs, n, dst, H, W, pad_value, S(stream));)
@@ -224,11 +233,13 @@ struct fce_net {
     hipGraphExec_t exec;
     const void* in;
     float* out;
+    unsigned long long* best;
     hipStream_t stream;
     int dtype, c;
     unsigned long long used;
   };
   static constexpr int kMaxGraphs = 4;
+  unsigned long long* cur_best = nullptr;  // best-class key output of the current forward (or null)
   std::vector<Captured> graphs;
   unsigned long long graph_clock = 0;
   // multi-stream capture: side streams + one event per op (+ fork), created on first capture
@@ -336,7 +347,8 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
       return psa_attention(x, op.heads, op.key_dim, op.head_dim, op.pe_w, op.pe_b, y, s);
     }
     case OP_CONV_DETECT: {
-      fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, op.part, op.strides[0]};
+      fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, op.part, op.strides[0],
+                       net->cur_best};
       return conv2d_detect(op.conv, x, op.w, op.b, e, s, op.tile);
     }
     case OP_DETECT: {
@@ -368,7 +380,7 @@ struct Access {
   int buf, c0, c1;
   bool write;
 };
-static constexpr int kBufPred = -2, kBufWs = -3;
+static constexpr int kBufPred = -2, kBufWs = -3, kBufBest = -4;
 
 static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access>& a) {
   a.clear();
@@ -398,6 +410,7 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
     case OP_CONV_DETECT:
       a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
       a.push_back({kBufPred, 2 * op.level + op.part, 2 * op.level + op.part + 1, true});
+      a.push_back({kBufBest, op.level, op.level + 1, true});  // box zeroes, cls maxes: keep them ordered
       break;
     case OP_DETECT:
       for (int i = 0; i < op.nl; ++i) a.push_back({op.box[i], 0, net->bufs[op.box[i]].c, false});
@@ -815,7 +828,13 @@ static int check_input(const fce_net* net, const fce_tensor* in) {
 }
 
 int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int graph, void* stream) {
+  return fce_net_forward_best(net, input, pred, nullptr, graph, stream);
+}
+
+int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
+                         void* stream) {
   FCE_CHECK(net && pred, "fce_net_forward: null argument");
+  net->cur_best = best;
   int st = check_input(net, input);
   if (st) return st;
   hipStream_t caller = S(stream);
@@ -844,7 +863,8 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
     }
     fce_net::Captured* hit = nullptr;
     for (fce_net::Captured& c : net->graphs)
-      if (c.in == input->data && c.out == pred && c.stream == s && c.dtype == input->dtype && c.c == input->c)
+      if (c.in == input->data && c.out == pred && c.best == best && c.stream == s && c.dtype == input->dtype &&
+          c.c == input->c)
         hit = &c;
     if (!hit) {
       if (int(net->graphs.size()) >= fce_net::kMaxGraphs) {  // evict the least recently replayed
@@ -867,7 +887,7 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
         (void)hipGraphDestroy(g);
         return fail(FCE_ERR_HIP, "fce_net_forward: hipGraphInstantiate failed");
       }
-      net->graphs.push_back({g, x, input->data, pred, s, input->dtype, input->c, 0});
+      net->graphs.push_back({g, x, input->data, pred, best, s, input->dtype, input->c, 0});
       hit = &net->graphs.back();
     }
     hit->used = ++net->graph_clock;

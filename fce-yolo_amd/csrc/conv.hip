@@ -142,6 +142,7 @@ struct ConvArgs {
   float* pred;
   int det_A, det_a0, det_nc, det_hw, det_w;
   float det_stride;
+  unsigned long long* det_best;  // per-anchor best-class key [N][A] (fce_detect_epi::best), or null
 };
 
 enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3, OUT_DFL = 4, OUT_CLS = 5 };
@@ -197,6 +198,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         const float ax = (float)(q % a.det_w) + 0.5f, ay = (float)(q / a.det_w) + 0.5f;
         const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
         float* o = a.pred + int64_t(n) * (4 + a.det_nc) * a.det_A + a.det_a0 + q;
+        if (a.det_best) a.det_best[int64_t(n) * a.det_A + a.det_a0 + q] = 0ull;  // the cls epilogue maxes into it
         o[0] = (x1 + x2) / 2.0f * a.det_stride;
         o[a.det_A] = (y1 + y2) / 2.0f * a.det_stride;
         o[int64_t(2) * a.det_A] = (x2 - x1) * a.det_stride;
@@ -206,6 +208,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
     return;
   }
   if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
+    // with det_best: the pixel's best class over this wave's couts (first maximum, like torch.max in
+    // utils/nms.py) as one key = score bits << 32 | ~class (scores >= 0: integer order = float order;
+    // ties -> the lower class), merged over the 4 cout groups by xor-shuffles, one atomic max per pixel
+    unsigned long long bk[RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) bk[p] = 0ull;
 #pragma unroll
     for (int r = 0; r < RC; ++r) {
       const int co0 = (cot0 + r) * 16 + grp * 4;
@@ -217,7 +225,28 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) o[int64_t(co0 + j) * a.det_A] = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+          if (co0 + j < a.cout) {
+            const float sc = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+            o[int64_t(co0 + j) * a.det_A] = sc;
+            const unsigned long long key =
+                (uint64_t(__float_as_uint(sc)) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(co0 + j));
+            bk[p] = key > bk[p] ? key : bk[p];
+          }
+      }
+    }
+    if (a.det_best) {
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        unsigned long long k = bk[p];
+        const unsigned long long k16 = __shfl_xor(k, 16);
+        k = k16 > k ? k16 : k;
+        const unsigned long long k32 = __shfl_xor(k, 32);
+        k = k32 > k ? k32 : k;
+        const int pix = pix_base + p * 16 + col;
+        if (grp == 0 && pix < a.P && k) {
+          const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+          atomicMax(a.det_best + int64_t(n) * a.det_A + a.det_a0 + q, k);
+        }
       }
     }
     return;
@@ -2725,6 +2754,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_hw = Ho * Wo;
   a.det_w = Wo;
   a.det_stride = det ? det->stride : 0.f;
+  a.det_best = det ? det->best : nullptr;
   const bool fast = d.cin % 32 == 0;
   int rc, rp;
   const int kind = tile >= 0 ? (tile >> 8) & 15 : -1;

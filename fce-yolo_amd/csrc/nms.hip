@@ -1,6 +1,8 @@
 // Non-maximum suppression on the device (reference ultralytics/utils/nms.py:13-166 with the predict
 // defaults multi_label=False, agnostic=False, classes=None; TorchNMS.nms :239-296; xywh2xyxy
-// utils/ops.py:224-240).  nms_best_class_kernel (all CUs) + one 1024-thread workgroup per image:
+// utils/ops.py:224-240).  nms_best_class_kernel (all CUs; skipped when the forward's Detect cls
+// epilogue already produced the per-anchor best-class keys, fce_nms_best) + one 1024-thread workgroup
+// per image:
 //   1. candidates: best class per anchor (first maximum), keep conf > conf_thres, compacted in anchor
 //      order with a block prefix sum; the class-offset xyxy box (cls * max_wh) and its area are
 //      formed here, where the anchor-ordered loads coalesce;
@@ -274,7 +276,8 @@ __global__ __launch_bounds__(256) void nms_best_class_kernel(const float* pred, 
   w.acls[a] = bj;
 }
 
-__global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int nc, int A, float conf_thres,
+__global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, const unsigned long long* bestk, int nc,
+                                                          int A, float conf_thres,
                                                           float iou_thres, int max_det, int max_nms, float max_wh,
                                                           char* ws, size_t ws_per_image, float* dets, int64_t* keep,
                                                           int32_t* counts, int stop) {
@@ -298,8 +301,14 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
     float best = -INFINITY;
     int bj = 0;
     if (a < A) {
-      best = w.aconf[a];
-      bj = w.acls[a];
+      if (bestk) {  // fused into the Detect cls epilogue: score bits << 32 | ~class
+        const unsigned long long k = bestk[int64_t(n) * A + a];
+        best = __uint_as_float(uint32_t(k >> 32));
+        bj = int(0xFFFFFFFFu - uint32_t(k));
+      } else {
+        best = w.aconf[a];
+        bj = w.acls[a];
+      }
     }
     const int flag = (a < A) && (best > conf_thres);
     const int pos = block_scan(flag, wsum, &s_total);
@@ -612,8 +621,9 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, int
   if (threadIdx.x == 0) counts[n] = s_kept;
 }
 
-int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_det, int max_nms, float max_wh,
-        void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s) {
+int nms(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou, int max_det,
+        int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
+        hipStream_t s) {
   FCE_CHECK(nc >= 1 && nc <= 65535 && A >= 0 && max_det >= 1 && max_nms >= 1, "nms: bad sizes");
   FCE_CHECK(max_nms <= REMOVED_CAP, "nms: max_nms > 32768 unsupported");
   FCE_CHECK(conf >= 0.f && conf <= 1.f && iou >= 0.f && iou <= 1.f, "nms: thresholds must be in [0, 1]");
@@ -622,10 +632,10 @@ int nms(const float* pred, int n, int nc, int A, float conf, float iou, int max_
   FCE_CHECK(ws && ws_bytes >= per * n, "nms: workspace too small");
   const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
   const int stop = stop_env ? atoi(stop_env) : 0;
-  if (A > 0)
+  if (A > 0 && !best)  // else the keys came from the Detect cls epilogue (fce_nms_best)
     FCE_LAUNCH(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);
-  FCE_LAUNCH(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, nc, A, conf, iou, max_det, max_nms, max_wh,
+  FCE_LAUNCH(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, best, nc, A, conf, iou, max_det, max_nms, max_wh,
                      static_cast<char*>(ws), per, dets, keep, counts, stop);
   return launch_status("nms_kernel");
 }

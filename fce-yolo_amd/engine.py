@@ -39,6 +39,12 @@ class Engine:
         self.anchors = N.lib().fce_net_num_anchors(self.be.net)
         self.nc = model.model[-1].nc
         self.pred = torch.empty((batch, 4 + self.nc, self.anchors), dtype=torch.float32, device=self.device)
+        self.best = self.new_best()
+
+    def new_best(self) -> torch.Tensor:
+        """A (batch, A) buffer for the per-anchor best-class keys the forward can emit for the NMS
+        (score bits << 32 | ~class, fce_detect_epi.best)."""
+        return torch.zeros((self.batch, self.anchors), dtype=torch.int64, device=self.device)
 
     def close(self):
         self.be.close()
@@ -60,11 +66,18 @@ class Engine:
             raise ValueError(f"Engine: input must be contiguous NCHW {(self.batch, 3, self.H, self.W)}")
         return N.Tensor(x.data_ptr(), _DT[x.dtype], N.NCHW, self.batch, 3, self.H, self.W, 3, 0)
 
-    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, graph: bool | None = None) -> torch.Tensor:
-        out = self.pred if out is None else out
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, graph: bool | None = None,
+                 best: torch.Tensor | None = None) -> torch.Tensor:
+        """Forward into `out` (default: self.pred, with its best-class keys in self.best).  `best`: a
+        new_best() buffer that receives the keys of this forward (for NMS(pred, best))."""
+        if out is None:
+            out, best = self.pred, self.best if best is None else best
+        if best is not None:
+            assert best.dtype == torch.int64 and tuple(best.shape) == (self.batch, self.anchors) and best.is_contiguous()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         g = self.graph if graph is None else graph
-        N.call("fce_net_forward", self.be.net, C.byref(self._in(x)), out.data_ptr(), int(bool(g)), stream)
+        N.call("fce_net_forward_best", self.be.net, C.byref(self._in(x)), out.data_ptr(),
+               best.data_ptr() if best is not None else None, int(bool(g)), stream)
         return out
 
     def profile(self, x: torch.Tensor, launches: bool = False):
@@ -132,13 +145,20 @@ class NMS:
         counts = buf[k + d:k + d + batch * 4].view(torch.int32)
         return keep, dets, counts
 
-    def __call__(self, pred: torch.Tensor):
+    def __call__(self, pred: torch.Tensor, best: torch.Tensor | None = None):
+        """`best`: the best-class keys the forward wrote with `pred` (Engine(..., best=)), which spares the
+        class arg-max pass over pred; the results are the same either way."""
         assert pred.is_contiguous() and pred.dtype == torch.float32 and tuple(pred.shape) == (
             self.batch, 4 + self.nc, self.anchors)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        N.call("fce_nms", pred.data_ptr(), self.batch, self.nc, self.anchors, self.conf, self.iou, self.max_det,
-               self.max_nms, float(self.max_wh), self.ws.data_ptr(), self.ws.numel(), self.dets.data_ptr(),
-               self.keep.data_ptr(), self.counts.data_ptr(), stream)
+        args = (self.batch, self.nc, self.anchors, self.conf, self.iou, self.max_det, self.max_nms,
+                float(self.max_wh), self.ws.data_ptr(), self.ws.numel(), self.dets.data_ptr(), self.keep.data_ptr(),
+                self.counts.data_ptr(), stream)
+        if best is not None:
+            assert best.dtype == torch.int64 and tuple(best.shape) == (self.batch, self.anchors)
+            N.call("fce_nms_best", pred.data_ptr(), best.data_ptr(), *args)
+        else:
+            N.call("fce_nms", pred.data_ptr(), *args)
         return self.dets, self.keep, self.counts
 
     def results(self):
@@ -176,6 +196,7 @@ class Pipeline:
         self.eng, self.depth, self.post = engine, depth, post
         dev = engine.device
         self.preds = [torch.empty_like(engine.pred) for _ in range(depth)]
+        self.bests = [engine.new_best() for _ in range(depth)]
         self.nms = [NMS(engine.batch, engine.anchors, engine.nc, dev, **nms_kw) for _ in range(depth)]
         self.side = torch.cuda.Stream(dev)
         self.fwd_done = [torch.cuda.Event() for _ in range(depth)]
@@ -189,11 +210,11 @@ class Pipeline:
         main = torch.cuda.current_stream(self.eng.device)
         if self.used[k]:
             main.wait_event(self.nms_done[k])  # pred[k] / nms[k] free again
-        self.eng(x, out=self.preds[k])
+        self.eng(x, out=self.preds[k], best=self.bests[k])
         self.fwd_done[k].record(main)
         self.side.wait_event(self.fwd_done[k])
         with torch.cuda.stream(self.side):
-            self.nms[k](self.preds[k])
+            self.nms[k](self.preds[k], self.bests[k])
             if self.post is not None:
                 self.post(k)
             self.nms_done[k].record(self.side)

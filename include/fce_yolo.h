@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 1
+#define FCE_ABI_VERSION 2
 
 /* status codes */
 #define FCE_OK 0
@@ -110,6 +110,10 @@ typedef struct fce_detect_epi {
   float* pred;
   int anchors, anchor_offset, nc, reg_max, part;
   float stride;
+  /* optional (NULL = off): per-anchor best-class key (n, anchors) uint64 = score bits << 32 | (~class),
+   * the argmax of utils/nms.py:91-104 (first maximum) produced by the cls epilogue with an atomic max;
+   * the box epilogue (part 0) of the same level zeroes it first.  fce_nms_best consumes it. */
+  unsigned long long* best;
 } fce_detect_epi;
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
                       const fce_detect_epi* e, void* stream);
@@ -190,6 +194,11 @@ size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 int fce_nms(const float* pred, int n, int nc, int anchors, float conf_thres, float iou_thres, int max_det,
             int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
             void* stream);
+/* fce_nms with the per-anchor best-class keys (fce_detect_epi::best) of the forward that wrote pred:
+ * the class arg-max pass over pred's nc rows (nms.py:91-104) is skipped.  Same results as fce_nms. */
+int fce_nms_best(const float* pred, const unsigned long long* best, int n, int nc, int anchors, float conf_thres,
+                 float iou_thres, int max_det, int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets,
+                 int64_t* keep, int32_t* counts, void* stream);
 
 /* ---------------------------------------------------------------- layout / dtype edges */
 /* dst = src with layout / dtype conversion (same n,c,h,w). */
@@ -225,6 +234,10 @@ int fce_net_num_anchors(const fce_net* net);
  * graph=1 captures the whole forward into a hipGraph on first use for these pointers and
  * replays it afterwards (re-captured if the pointers change). */
 int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int graph, void* stream);
+/* fce_net_forward that also writes the per-anchor best-class keys (batch, A) uint64 for fce_nms_best
+ * (best may be NULL).  fce_net_profile runs with the keys of the most recent forward. */
+int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
+                         void* stream);
 /* Eager run in which every kernel is launched with its own (start, stop) event pair
  * (hipExtLaunchKernelGGL): ms[i] = summed kernel execution time of op i, launches[i] (nullable) = its
  * kernel count (cap entries each). */

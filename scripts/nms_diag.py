@@ -24,7 +24,7 @@ pred = eng(x).clone()
 nms = NMS(B, eng.anchors, eng.nc, dev)
 ncand = (pred[:, 4:].amax(1) > 0.25).sum(1)
 print("candidates per image: min", int(ncand.min()), "max", int(ncand.max()), "of", eng.anchors, flush=True)
-for stop in ("1", "2", "5", "3", "0"):
+for stop in ("1", "2", "5", "3", "0", "7", "8"):
     os.environ["FCE_NMS_STOP"] = stop
     for _ in range(3):
         nms(pred)

@@ -313,6 +313,58 @@ def test_nms_clustered_suppression_chains(seed, device):
             assert np.array_equal(dets[b].cpu().numpy(), od[b]), (iou, max_det, b)
 
 
+@pytest.mark.parametrize("case", ["bench_like", "unbanded", "one_class_heavy"])
+def test_nms_top_selection_and_class_buckets(case, device):
+    """The large-candidate-set paths against the oracle: top-1024 selection (MSB radix select on tied
+    scores) with the full-sort fallback, and the class-bucketed kept lists (exact only inside the class
+    bands; `unbanded` breaks the band condition with max_wh below the box extent)."""
+    rng = np.random.default_rng(11)
+    B, A, nc = 3, 8400, 80
+    p = np.zeros((B, 4 + nc, A), np.float32)
+    for b in range(B):
+        p[b, 0:2] = rng.random((2, A)) * 640
+        p[b, 2:4] = rng.random((2, A)) * 120 + 8
+        if case == "one_class_heavy":  # 2 classes, clustered: heavy suppression, long class lists
+            cls = rng.integers(0, 2, A)
+            c = rng.random((20, 2)) * 600 + 20
+            k = rng.integers(0, 20, A)
+            p[b, 0:2] = (c[k] + rng.normal(0, 8, (A, 2))).T
+        else:
+            cls = rng.integers(0, nc, A)
+        sc = np.where(rng.random(A) < 0.7, 1.0, rng.random(A)).astype(np.float32)  # saturated, like the bench
+        p[b, 4 + cls, np.arange(A)] = sc
+    max_wh = 64.0 if case == "unbanded" else 7680.0
+    pt = torch.from_numpy(p).to(device)
+    for iou, max_det in ((0.7, 300), (0.45, 300), (0.7, 1000)):
+        dets, keep = non_max_suppression(pt, 0.25, iou, max_det, max_wh=max_wh, return_idxs=True)
+        od, ok = nms_oracle.non_max_suppression(p, 0.25, iou, max_det=max_det, max_wh=max_wh)
+        for b in range(B):
+            assert np.array_equal(keep[b].cpu().numpy(), ok[b]), (case, iou, max_det, b)
+            assert np.array_equal(dets[b].cpu().numpy(), od[b]), (case, iou, max_det, b)
+
+
+def test_fused_best_class_keys_match_pred_and_nms(device):
+    """The cls epilogue's per-anchor best-class keys (atomic max, box epilogue zeroes) equal torch.max over
+    the pred rows (first maximum), and the NMS fed with them equals the NMS that does its own arg-max."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    B, S = 4, 320
+    eng = Engine(model, B, S, device)
+    x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(77)).half().to(device)
+    for graph in (False, True):
+        best = eng.new_best().fill_(-1)
+        pred = eng(x, out=torch.empty_like(eng.pred), best=best, graph=graph)
+        torch.cuda.synchronize()
+        sc, cl = pred[:, 4:].max(1)
+        kb = best.cpu().numpy().view(np.uint64)
+        assert np.array_equal((kb >> np.uint64(32)).astype(np.uint32), sc.cpu().numpy().view(np.uint32))
+        assert np.array_equal((np.uint64(0xFFFFFFFF) - (kb & np.uint64(0xFFFFFFFF))).astype(np.int64), cl.cpu().numpy())
+        n1, n2 = NMS(B, eng.anchors, eng.nc, device), NMS(B, eng.anchors, eng.nc, device)
+        n1(pred)
+        n2(pred, best)
+        torch.cuda.synchronize()
+        assert torch.equal(n1.buf, n2.buf)
+
+
 def test_pipeline_overlap_matches_sequential(device):
     """engine.Pipeline (forward i+1 overlapping NMS i, double-buffered) gives every batch exactly the
     sequential forward + NMS result."""
