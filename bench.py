@@ -192,11 +192,13 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    sp.flush()
     _trace_marker()
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    sp.flush()  # the last batch's NMS (+ gather) is inside the timed region
     barrier()
     el = time.perf_counter() - t0
     _trace_marker()

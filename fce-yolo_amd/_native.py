@@ -126,6 +126,9 @@ _SIGS = {
     "fce_net_num_anchors": (_I, [_P]),
     "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),
     "fce_net_forward_best": (_I, [_P, _PT, _P, _P, _I, _P]),
+    "fce_net_fork_hint": (_I, [_P]),
+    "fce_net_set_fork": (_I, [_P, _I]),
+    "fce_net_wait_fork": (_I, [_P, _P]),
     "fce_net_profile": (_I, [_P, _PT, _P, _P, _P, _I, _P]),
     "fce_net_num_ops": (_I, [_P]),
     "fce_net_op_variant": (_I, [_P, _I]),

@@ -240,6 +240,11 @@ struct fce_net {
   };
   static constexpr int kMaxGraphs = 4;
   unsigned long long* cur_best = nullptr;  // best-class key output of the current forward (or null)
+  // fork point: after op fork_op of a direct-launch forward, mid_ev is recorded on the forward's stream
+  // (a side stream can start concurrent work -- the previous batch's NMS -- where the forward leaves
+  // CUs idle); with graph replay, multiple streams or fork_op < 0 it is recorded at the end instead
+  int fork_op = -1;
+  hipEvent_t mid_ev = nullptr;
   std::vector<Captured> graphs;
   unsigned long long graph_clock = 0;
   // multi-stream capture: side streams + one event per op (+ fork), created on first capture
@@ -283,6 +288,7 @@ struct fce_net {
   ~fce_net() {
     release();
     drop_streams();
+    if (mid_ev) (void)hipEventDestroy(mid_ev);
   }
 
   fce_tensor view(int id, int coff, int c) const {
@@ -364,10 +370,11 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
   return fail(FCE_ERR_INVALID, "unknown op");
 }
 
-int run_all(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s) {
-  for (const OpDesc& op : net->ops) {
-    int st = run_op(net, op, input, pred, s);
+int run_all(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s, bool fork = false) {
+  for (size_t i = 0; i < net->ops.size(); ++i) {
+    int st = run_op(net, net->ops[i], input, pred, s);
     if (st) return st;
+    if (fork && int(i) == net->fork_op) FCE_HIP_CHECK(hipEventRecord(net->mid_ev, s));
   }
   return FCE_OK;
 }
@@ -555,6 +562,35 @@ fce_net* fce_net_create(void) {
   }
 }
 void fce_net_destroy(fce_net* net) { delete net; }
+
+int fce_net_fork_hint(const fce_net* net) {
+  // the op after which the forward runs at its coarsest resolution (stride 32): from there on the
+  // forward's kernels are small and leave most CUs idle
+  if (!net) return -1;
+  int best = -1, shift = -1;
+  for (size_t i = 0; i < net->ops.size(); ++i) {
+    const OpDesc& op = net->ops[i];
+    if (op.kind == OP_CONV && op.out >= 0 && net->bufs[op.out].shift > shift) {
+      shift = net->bufs[op.out].shift;
+      best = int(i);
+    }
+  }
+  return best;
+}
+
+int fce_net_set_fork(fce_net* net, int op) {
+  FCE_CHECK(net && op >= -1 && op < int(net->ops.size()), "fce_net_set_fork: bad op");
+  if (!net->mid_ev) FCE_HIP_CHECK(hipEventCreateWithFlags(&net->mid_ev, hipEventDisableTiming));
+  net->fork_op = op;
+  net->drop_graph();
+  return FCE_OK;
+}
+
+int fce_net_wait_fork(fce_net* net, void* stream) {
+  FCE_CHECK(net && net->mid_ev, "fce_net_wait_fork: call fce_net_set_fork first");
+  FCE_HIP_CHECK(hipStreamWaitEvent(S(stream), net->mid_ev, 0));
+  return FCE_OK;
+}
 
 int fce_net_add_buffer(fce_net* net, int c, int shift, int dtype) {
   FCE_CHECK(net && c > 0 && shift >= 0 && shift <= 8 && (dtype == FCE_F16 || dtype == FCE_F32),
@@ -845,8 +881,10 @@ int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, uns
       // spreads the op DAG over that many net-owned streams
       const char* ns = getenv("FCE_STREAMS");
       const int nstreams = std::max(1, std::min(8, ns ? atoi(ns) : 1));
-      if (nstreams == 1) return run_all(net, *input, pred, caller);
-      return run_all_streams(net, *input, pred, caller, nstreams);
+      const bool mid = net->mid_ev && net->fork_op >= 0 && nstreams == 1;
+      st = nstreams == 1 ? run_all(net, *input, pred, caller, mid) : run_all_streams(net, *input, pred, caller, nstreams);
+      if (!st && net->mid_ev && !mid) FCE_HIP_CHECK(hipEventRecord(net->mid_ev, caller));
+      return st;
     }
     // hipGraph: one linear capture (the legacy null stream cannot be captured, so the net then
     // captures and replays on a stream of its own, ordered against the caller's with events)
@@ -892,6 +930,7 @@ int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, uns
     }
     hit->used = ++net->graph_clock;
     FCE_HIP_CHECK(hipGraphLaunch(hit->exec, s));
+    if (net->mid_ev) FCE_HIP_CHECK(hipEventRecord(net->mid_ev, s));
     if (s != caller) {
       FCE_HIP_CHECK(hipEventRecord(net->join_ev[1], s));
       FCE_HIP_CHECK(hipStreamWaitEvent(caller, net->join_ev[1], 0));

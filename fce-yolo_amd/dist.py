@@ -162,8 +162,14 @@ class ShardedPredictor:
             raise ValueError(f"rank {self.rank}: shard of {self.batch} images expected, got {x.shape[0]}")
         return self.pipe.submit(x)
 
+    def flush(self):
+        """Issue the last pending NMS (+ gather); call before timing / synchronising on a batch's results."""
+        self.pipe.flush()
+
     def results(self, k: int):
         """(dets, keep) per image of the whole global batch, in the unsharded order."""
+        if k == self.pipe.pending:
+            self.pipe.flush()
         self.pipe.nms_done[k].synchronize()
         g = self.gathered[k] if self.world > 1 else self.pipe.nms[k].buf
         return unpack_gathered(g, self.sizes, self.max_det)

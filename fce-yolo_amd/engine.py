@@ -180,20 +180,25 @@ def non_max_suppression(pred: torch.Tensor, conf_thres=0.25, iou_thres=0.7, max_
 
 
 class Pipeline:
-    """Batch pipeline: forward of batch i+1 overlaps the NMS of batch i.
+    """Batch pipeline: the NMS of batch i overlaps the forward of batch i+1.
 
-    The forward runs on the caller's stream into one of `depth` pred buffers; the NMS of that buffer runs
-    on a side stream after an event.  A buffer (and its NMS outputs) is reused only after the NMS that
-    read it has finished (event wait on the caller's stream), so every batch gets exactly the forward +
-    NMS of the sequential path — the NMS latency (one workgroup per image) just hides under the next
-    forward.  `submit(x)` returns the slot whose `NMS` object holds that batch's results once
-    `wait(slot)` (or a device sync) has passed.
+    The forward runs on the caller's stream into one of `depth` pred buffers (+ best-class keys); the NMS
+    of that buffer runs on a side stream.  A buffer (and its NMS outputs) is reused only after the NMS
+    that read it has finished (event wait on the caller's stream), so every batch gets exactly the
+    forward + NMS of the sequential path.
+
+    With `defer` (default) the NMS of batch i is issued only after the forward of batch i+1 has been
+    enqueued, and waits for that forward's fork point (``fce_net_set_fork`` at ``fce_net_fork_hint``: the
+    first op at stride 32): it then runs while the forward is in its small coarse-resolution layers that
+    leave most CUs idle, instead of competing with the full-width early layers.  `flush()` issues the
+    last pending NMS; `wait` / `results` flush when needed.  `submit(x)` returns the slot whose `NMS`
+    object holds that batch's results once `wait(slot)` (or a device sync after `flush()`) has passed.
     """
 
-    def __init__(self, engine: Engine, depth: int = 2, post=None, **nms_kw):
+    def __init__(self, engine: Engine, depth: int = 2, post=None, defer: bool = True, **nms_kw):
         """`post(k)`, if given, runs on the side stream right after slot k's NMS (e.g. the multi-GPU gather
         of its outputs, dist.ShardedPredictor); the slot is reused only after it too has finished."""
-        self.eng, self.depth, self.post = engine, depth, post
+        self.eng, self.depth, self.post, self.defer = engine, depth, post, defer
         dev = engine.device
         self.preds = [torch.empty_like(engine.pred) for _ in range(depth)]
         self.bests = [engine.new_best() for _ in range(depth)]
@@ -202,32 +207,57 @@ class Pipeline:
         self.fwd_done = [torch.cuda.Event() for _ in range(depth)]
         self.nms_done = [torch.cuda.Event() for _ in range(depth)]
         self.used = [False] * depth
+        self.pending = None  # slot whose NMS is not issued yet (defer)
         self.i = 0
+        if defer:
+            N.call("fce_net_set_fork", engine.net, N.lib().fce_net_fork_hint(engine.net))
 
-    def submit(self, x: torch.Tensor) -> int:
-        k = self.i % self.depth
-        self.i += 1
-        main = torch.cuda.current_stream(self.eng.device)
-        if self.used[k]:
-            main.wait_event(self.nms_done[k])  # pred[k] / nms[k] free again
-        self.eng(x, out=self.preds[k], best=self.bests[k])
-        self.fwd_done[k].record(main)
+    def _issue_nms(self, k: int, fork: bool):
         self.side.wait_event(self.fwd_done[k])
+        if fork:  # the next forward has reached its coarse layers
+            N.call("fce_net_wait_fork", self.eng.net, self.side.cuda_stream)
         with torch.cuda.stream(self.side):
             self.nms[k](self.preds[k], self.bests[k])
             if self.post is not None:
                 self.post(k)
             self.nms_done[k].record(self.side)
+
+    def submit(self, x: torch.Tensor) -> int:
+        k = self.i % self.depth
+        self.i += 1
+        main = torch.cuda.current_stream(self.eng.device)
+        if self.pending == k:  # depth 1: this slot's NMS must be issued before the slot is reused
+            self.flush()
+        if self.used[k]:
+            main.wait_event(self.nms_done[k])  # pred[k] / nms[k] free again
+        self.eng(x, out=self.preds[k], best=self.bests[k])
+        self.fwd_done[k].record(main)
         self.used[k] = True
+        if not self.defer:
+            self._issue_nms(k, False)
+            return k
+        if self.pending is not None:
+            self._issue_nms(self.pending, True)
+        self.pending = k
         return k
+
+    def flush(self):
+        """Issue the NMS still pending (deferred mode) without waiting for another forward."""
+        if self.pending is not None:
+            k, self.pending = self.pending, None
+            self._issue_nms(k, False)
 
     def wait(self, k: int | None = None):
         """Make the caller's stream wait for the NMS of slot k (all slots when None)."""
+        if k is None or k == self.pending:
+            self.flush()
         main = torch.cuda.current_stream(self.eng.device)
         for j in range(self.depth) if k is None else (k,):
             if self.used[j]:
                 main.wait_event(self.nms_done[j])
 
     def results(self, k: int):
+        if k == self.pending:
+            self.flush()
         self.nms_done[k].synchronize()
         return self.nms[k].results()

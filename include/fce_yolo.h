@@ -238,6 +238,13 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
  * (best may be NULL).  fce_net_profile runs with the keys of the most recent forward. */
 int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
                          void* stream);
+/* Fork point for overlapping work with the forward (SURVEY §8(e) double-buffered batches): after
+ * fce_net_set_fork(net, op), every direct-launch forward records an event after op `op` (at the end
+ * with graph replay / multiple streams / op = -1), and fce_net_wait_fork(net, stream) makes `stream`
+ * wait for the most recent such event.  fce_net_fork_hint = the first op at the coarsest resolution. */
+int fce_net_fork_hint(const fce_net* net);
+int fce_net_set_fork(fce_net* net, int op);
+int fce_net_wait_fork(fce_net* net, void* stream);
 /* Eager run in which every kernel is launched with its own (start, stop) event pair
  * (hipExtLaunchKernelGGL): ms[i] = summed kernel execution time of op i, launches[i] (nullable) = its
  * kernel count (cap entries each). */
