@@ -1295,6 +1295,9 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
   for (int r = 0; r < RC; ++r)
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 af[RC];  // A fragments of the current K-step (prefetched one step ahead in the tap loop)
+#pragma unroll
+  for (int r = 0; r < RC; ++r) af[r] = wfrag[r][0];
   const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   // Staging: NL pieces per thread.  When they fit in registers (NL <= 8) the next stage's global
@@ -1349,9 +1352,14 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int ky = tap / 3, kx = tap - ky * 3;
-        h8 af[RC], bf[RP];
+        h8 bf[RP];
+        // A fragments one K-step ahead (the last step of the last chunk re-reads its own; weights only,
+        // no LDS hazard across the staging barrier): the L2 latency hides under this step's MFMAs
+        const int ks = (c0 + k) * 9 + tap + 1;
+        const int ksn = ks < spt * 9 ? ks : ks - 1;
+        h8 an[RC];
 #pragma unroll
-        for (int r = 0; r < RC; ++r) af[r] = wfrag[r][((c0 + k) * 9 + tap) * 64];
+        for (int r = 0; r < RC; ++r) an[r] = wfrag[r][ksn * 64];
 #pragma unroll
         for (int p = 0; p < RP; ++p) {
           const int ry = (wr * RP + p) * S + ky;
@@ -1363,6 +1371,8 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 #pragma unroll
           for (int p = 0; p < RP; ++p)
             acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < RC; ++r) af[r] = an[r];
       }
     }
   }
@@ -2363,9 +2373,12 @@ static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, 
 static constexpr size_t tile3_lds(int s, int rp, int cw, int kp) {
   return size_t(((4 / cw) * rp - 1) * s + 3) * (15 * s + 3) * 4 * kp * 16;
 }
+// rp = 8 (8 output rows per wave: every A fragment read from L2 feeds 8 MFMAs, the m/l-scale 3x3 convs
+// are L2-bound at rp <= 4) only with rc >= 2 and the couts split over 2 / 4 waves
 static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
-  return (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4) && (cw == 1 || cw == 2 || cw == 4) &&
-         (kp == 1 || kp == 2) && rc * rp <= 16 && tile3_lds(s, rp, cw, kp) <= 80 * 1024;
+  return (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && rc >= 2 && cw >= 2)) &&
+         (cw == 1 || cw == 2 || cw == 4) && (kp == 1 || kp == 2) && rc * rp <= 32 &&
+         tile3_lds(s, rp, cw, kp) <= 80 * 1024;
 }
 
 // Register tiles a dense conv may run with, encoded rc | rp << 4, or depthwise kernel variants,
@@ -2441,7 +2454,7 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
         for (int rc : {1, 2, 4}) {
           const int cb = (1 << cwl) * rc;
           if (cb > 1 && (cb >> 1) >= cotiles) continue;
-          for (int rp : {1, 2, 4})
+          for (int rp : {1, 2, 4, 8})
             if (n < cap && tile3_ok(d.stride, rc, rp, 1 << cwl, kp))
               out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14);
         }
@@ -2471,8 +2484,14 @@ static void launch_tile3_rc(const ConvArgs& a, int rp, int cw, int kp, dim3 grid
     launch_tile3_w<S, RC, 1>(a, cw, kp, grid, s);
   else if (rp == 2)
     launch_tile3_w<S, RC, 2>(a, cw, kp, grid, s);
-  else
+  else if (rp == 4)
     launch_tile3_w<S, RC, 4>(a, cw, kp, grid, s);
+  else if constexpr (RC >= 2) {  // rp == 8: cw 2 / 4 only (tile3_ok)
+    if (cw == 2)
+      kp == 1 ? launch_tile3_k<S, RC, 8, 2, 1>(a, grid, s) : launch_tile3_k<S, RC, 8, 2, 2>(a, grid, s);
+    else
+      kp == 1 ? launch_tile3_k<S, RC, 8, 4, 1>(a, grid, s) : launch_tile3_k<S, RC, 8, 4, 2>(a, grid, s);
+  }
 }
 
 template <int S>
@@ -2597,15 +2616,22 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     const size_t shm = size_t(x.c) * d.k * d.k * coutT * sizeof(float);
     const int PX = coutT <= 32 ? 2 : 1;  // measured: PX 2 beats 4 (occupancy) and 1 (reuse) at cout 16
     const char* sv = getenv("FCE_STEM_VALU");  // diagnostics: the fp32 VALU stem instead of MFMA
+    // the staged rows exceed 64 KiB above W = 1168 (imgsz 1280: 70 KiB): gfx950 LDS opt-in up to 160 KiB
     if (stem_mfma_ok(d) && d.stride == 2 && x.c == d.cin && d.cout % 16 == 0 && x.w % 8 == 0 &&
-        size_t(x.c) * 9 * (x.w + 16) * 2 + 16 <= 64 * 1024 && !(sv && atoi(sv))) {
+        size_t(x.c) * 9 * (x.w + 16) * 2 + 16 <= 160 * 1024 && !(sv && atoi(sv))) {
       const size_t lds = size_t(x.c) * 9 * (x.w + 16) * sizeof(_Float16) + 16;  // + the dummy staging slot
-      FCE_CHECK(lds <= 64 * 1024, "stem conv: input rows do not fit in LDS");
       const int64_t blocks2 = int64_t(x.n) * ((Ho + 3) / 4);
       FCE_CHECK(blocks2 < (int64_t(1) << 31), "stem conv: input too large");
       const _Float16* wfr = reinterpret_cast<const _Float16*>(static_cast<const char*>(w) + stem_fp32_bytes(d));
       const int rc = d.cout / 16;
-#define STEMM(T, RC) FCE_LAUNCH((stem_mfma_kernel<T, RC>), dim3(unsigned(blocks2)), dim3(256), lds, s, a, wfr)
+#define STEMM(T, RC)                                                                                          \
+  do {                                                                                                        \
+    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_mfma_kernel<T, RC>),     \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==    \
+                            hipSuccess;                                                                       \
+    if (!big && lds > 64 * 1024) return fail(FCE_ERR_HIP, "stem conv: cannot opt in to >64 KiB LDS");        \
+    FCE_LAUNCH((stem_mfma_kernel<T, RC>), dim3(unsigned(blocks2)), dim3(256), lds, s, a, wfr);                \
+  } while (0)
 #define STEMM_T(T)          \
   do {                      \
     if (rc == 1)            \

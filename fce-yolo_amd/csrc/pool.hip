@@ -170,7 +170,10 @@ int maxpool_chain(const fce_tensor& x, const fce_tensor& y1, const fce_tensor& y
   const int64_t total = int64_t(x.n) * x.h * x.w * (x.c / 8);
   if (total == 0) return FCE_OK;
   const size_t lds = (size_t(4) * x.h * x.w + 1) * sizeof(h8);  // 4 planes + the staging dummy
-  if (lds <= 64 * 1024 && int64_t(x.n) * (x.c / 8) < (int64_t(1) << 31)) {  // H*W <= 1024 (imgsz <= 1024)
+  // > 64 KiB (the 40 x 40 SPPF map at imgsz 1280) needs the gfx950 LDS opt-in (up to 160 KiB)
+  static const bool lds_big = hipFuncSetAttribute(reinterpret_cast<const void*>(&maxpool_chain_lds_kernel),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (lds <= (lds_big ? 160 : 64) * 1024 && int64_t(x.n) * (x.c / 8) < (int64_t(1) << 31)) {  // H*W <= 2560
     FCE_LAUNCH(maxpool_chain_lds_kernel, dim3(x.n * (x.c / 8)), dim3(256), lds, s, a);
     return launch_status("maxpool_chain_lds_kernel");
   }
