@@ -40,7 +40,7 @@ from fce_yolo_amd.weights import seeded_state_dict  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFS = 2500.0  # dense fp16 MFMA (no sparsity)
 RIDGE = MFMA_F16_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
-PMC_TRAFFIC = Path(__file__).resolve().parent / "profiles" / "pmc_traffic.json"
+PROFILES = Path(__file__).resolve().parent / "profiles"
 
 
 def _trace_marker():
@@ -50,11 +50,16 @@ def _trace_marker():
     torch.cuda._sleep(64)
 
 
-def _pmc_traffic(family):
-    """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (FETCH_SIZE x2 +
-    WRITE_SIZE, gfx950 correction; scripts/gpu_pmc.sh), or None."""
+def pmc_path(model: str, batch: int, imgsz: int) -> Path:
+    """The committed rocprofv3 PMC summary of THIS config (scripts/gpu_pmc.sh + pmc_summary.py)."""
+    return PROFILES / f"pmc_{Path(model).stem}_b{batch}_s{imgsz}.json"
+
+
+def _pmc_family(path: Path, family):
+    """The PMC summary's per-launch entry for `family` (FETCH_SIZE x2 + WRITE_SIZE with the gfx950
+    correction; MFMA counters when that pass was collected), or None."""
     try:
-        return float(json.loads(PMC_TRAFFIC.read_text())["families"][family]["hbm_bytes"])
+        return json.loads(path.read_text())["families"][family]
     except (OSError, KeyError, ValueError, TypeError):
         return None
 
@@ -115,8 +120,13 @@ def predict_rate(model, B: int, S: int, dev, steps: int):
                       f"{S}x{S} + forward + NMS + scale_boxes + results to host, {steps} batches"}
 
 
-def cpu_baseline(model_name: str, imgsz: int, seconds: float):
-    """The oracle (PyTorch-CPU fp32 restatement of the reference forward) on the host cores."""
+def cpu_baseline(model_name: str, imgsz: int, seconds: float, batch: int = 32):
+    """The oracle (PyTorch-CPU fp32 restatement of the reference forward) on the host cores, with the
+    BASELINE.md §2 protocol's batch (bs=32 on the headline config): one bs=1 warm-up, then whole bs=`batch`
+    forwards until `seconds` have passed (at least one), images/s from the median batch time; a bs=1
+    rate from the remaining time is reported beside it."""
+    import statistics
+
     from oracle import fce_oracle as O
     from oracle.parse import parse
 
@@ -124,23 +134,31 @@ def cpu_baseline(model_name: str, imgsz: int, seconds: float):
     cpu_model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in cpu_model.state_dict().items()], 0))
     layers, save, _ = parse(cpu_model.yaml)
     sd = O.cast_sd(O.fuse_state_dict(cpu_model.state_dict()), torch.float32)
-    x = torch.rand(1, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(0))
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.rand(1, 3, imgsz, imgsz, generator=g)
+    xb = torch.rand(batch, 3, imgsz, imgsz, generator=g)
     with torch.inference_mode():
-        O.forward(layers, save, sd, x)  # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            O.forward(layers, save, sd, x)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= seconds or n >= 2000:
-                break
+        O.forward(layers, save, sd, x1)  # warm-up
+        t_start = time.perf_counter()
+        times = []
+        while not times or (time.perf_counter() - t_start < seconds * 0.75 and len(times) < 5):
+            t0 = time.perf_counter()
+            O.forward(layers, save, sd, xb)
+            times.append(time.perf_counter() - t0)
+        n1, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t_start < seconds and n1 < 200:
+            O.forward(layers, save, sd, x1)
+            n1 += 1
+        el1 = time.perf_counter() - t1
+    med = statistics.median(times)
     return {
-        "value": round(n / el, 3),
+        "value": round(batch / med, 3),
         "unit": "images/sec",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": f"oracle fp32 forward of {model_name} @ {imgsz}x{imgsz}, bs=1, {n} images in {el:.1f} s "
-        f"(1 warm-up), torch {torch.__version__} CPU",
+        "sample": f"oracle fp32 forward of {model_name} @ {imgsz}x{imgsz}, bs={batch}: {len(times)} batch(es), "
+        f"median {med:.2f} s/batch (1 bs=1 warm-up), torch {torch.__version__} CPU",
+        "bs1_images_per_sec": round(n1 / el1, 3) if n1 else None,
     }
 
 
@@ -254,9 +272,13 @@ def main():
         ach = dbytes / dn / (dms / dn * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    tr = _pmc_traffic(dname)
-    roof["traffic"] = None if tr is None else round(tr / 1e6, 3)
-    roof["traffic_unit"] = "MB/launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_traffic.json)"
+    pp = pmc_path(a.model, B, S)
+    pf = _pmc_family(pp, dname)
+    roof["traffic"] = None if pf is None else round(float(pf["hbm_bytes"]) / 1e6, 3)
+    roof["traffic_unit"] = f"MB/launch (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, {pp.relative_to(ROOT)})"
+    if pf is not None and "mfma_tflops" in pf:  # MFMA counter pass of the same config (profiled clocks)
+        roof["mfma_counter"] = {"tflops": pf["mfma_tflops"], "frac": pf["mfma_frac"],
+                                "source": "SQ_INSTS_VALU_MFMA_MOPS_F16 x 512 / kernel time, rocprofv3 pass"}
     roof["kernel"] = dname
     roof["launches_per_step"] = dn
     roof["kernel_ms_per_step"] = round(dms, 4)
@@ -294,7 +316,7 @@ def main():
     if rank == 0 and world == 1 and a.predict_steps > 0:
         out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds, B)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -80,12 +80,24 @@ class CoordDesc(C.Structure):
     ]
 
 
+class C3k2Desc(C.Structure):
+    _fields_ = [
+        ("cin", C.c_int),
+        ("c", C.c_int),
+        ("c_mid", C.c_int),
+        ("cout", C.c_int),
+        ("w", C.c_void_p * 4),
+        ("b", C.c_void_p * 4),
+    ]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _SZ = C.c_size_t
 _PT = C.POINTER(Tensor)
 _PCD = C.POINTER(ConvDesc)
 _PCO = C.POINTER(CoordDesc)
+_PC3 = C.POINTER(C3k2Desc)
 
 _SIGS = {
     "fce_last_error": (C.c_char_p, []),
@@ -102,6 +114,9 @@ _SIGS = {
     "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),
     "fce_weighted_add": (_I, [_PT, _I, _P, _I, _I, _I, _PT, _P]),
     "fce_coord_workspace_bytes": (_SZ, [_PCO, _I, _I, _I]),
+    "fce_c3k2_supported": (_I, [_PC3]),
+    "fce_c3k2": (_I, [_PC3, _PT, _PT, _P]),
+    "fce_net_add_c3k2": (_I, [_P, _PC3, _I, _I, _I, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

@@ -60,6 +60,7 @@ class EagerBackend:
     """Runs every op immediately (drop-in nn.Module path)."""
 
     shape_only = False
+
     def __init__(self, device: torch.device):
         self.device = device
         self.stream = torch.cuda.current_stream(device).cuda_stream
@@ -134,6 +135,9 @@ class EagerBackend:
         fn = ("fce_bicoordcrossatt", "fce_coordatt", "fce_coordcrossatt")[kind]
         N.call(fn, C.byref(desc), C.byref(self.t(x)), C.byref(self.t(y)), ws.data_ptr(), nb, self.stream)
         self._keep = ws  # keep alive until the stream has consumed it (caching allocator is stream-ordered)
+
+    def c3k2(self, desc: N.C3k2Desc, x: View, y: View):
+        N.call("fce_c3k2", C.byref(desc), C.byref(self.t(x)), C.byref(self.t(y)), self.stream)
 
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         N.call("fce_psa_attention", C.byref(self.t(qkv)), heads, kd, hd, pe_w, pe_b, C.byref(self.t(y)), self.stream)
@@ -259,6 +263,9 @@ class NetBackend:
     def coord(self, kind: int, desc: N.CoordDesc, x: View, y: View):
         x = self.materialize(x)
         N.call("fce_net_add_coord", self.net, kind, C.byref(desc), x.buf, x.coff, y.buf, y.coff)
+
+    def c3k2(self, desc: N.C3k2Desc, x: View, y: View):
+        N.call("fce_net_add_c3k2", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff)
 
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         assert qkv.coff == 0 and qkv.c == qkv.cstride

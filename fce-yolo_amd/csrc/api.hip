@@ -42,6 +42,9 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
         int max_nms, float max_wh,
         void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
 
+bool c3k2_fused_ok(const fce_c3k2_desc& d);
+int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
+
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
 int scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* sc, hipStream_t s);
 
@@ -103,6 +106,11 @@ int fce_conv2d_variant(const fce_conv_desc* d, const fce_tensor* x, const void* 
                        const fce_tensor* res, const fce_tensor* y, int variant, void* stream) {
   FCE_CHECK(d && x && w && bias && y, "fce_conv2d_variant: null argument");
   FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream), variant);)
+}
+int fce_c3k2_supported(const fce_c3k2_desc* d) { return d && c3k2_fused_ok(*d) ? 1 : 0; }
+int fce_c3k2(const fce_c3k2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
+  FCE_CHECK(d && x && y, "fce_c3k2: null argument");
+  FCE_GUARD(return c3k2_fused(*d, *x, *y, S(stream));)
 }
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
                       const fce_detect_epi* e, void* stream) {
@@ -178,7 +186,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2 };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -206,6 +214,7 @@ struct OpDesc {
   float strides[4] = {0, 0, 0, 0};
   int reg_max = 16;
   int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT
+  fce_c3k2_desc c3k2{};              // OP_C3K2
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
 };
 
@@ -352,6 +361,10 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
       fce_tensor y = net->view(op.out, op.out_coff, op.heads * op.head_dim);
       return psa_attention(x, op.heads, op.key_dim, op.head_dim, op.pe_w, op.pe_b, y, s);
     }
+    case OP_C3K2: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.c3k2.cout);
+      return c3k2_fused(op.c3k2, x, y, s);
+    }
     case OP_CONV_DETECT: {
       fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, op.part, op.strides[0],
                        net->cur_best};
@@ -413,6 +426,10 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
     case OP_PSA:
       a.push_back({op.in, op.in_coff, op.in_coff + op.in_c, false});
       a.push_back({op.out, op.out_coff, op.out_coff + op.heads * op.head_dim, true});
+      break;
+    case OP_C3K2:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.c3k2.cin, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.c3k2.cout, true});
       break;
     case OP_CONV_DETECT:
       a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
@@ -530,6 +547,19 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       *bytes = px * op.coord.inp * 2 * 2 + px * op.coord.oup * 2;  // 2 reads (pool, gate) + 1 write
       const double L = double(net->H >> net->bufs[op.in].shift) + double(net->W >> net->bufs[op.in].shift);
       *flops = 2.0 * N * (3.0 * op.coord.mid * op.coord.inp * L + op.coord.oup * op.coord.mid * L);
+      break;
+    }
+    case OP_C3K2: {  // one read of x, one write of y, the four convs' weights
+      const fce_c3k2_desc& d = op.c3k2;
+      *name = "c3k2_fused";
+      const double px = N * hw(op.in);
+      const fce_conv_desc cs[4] = {{d.cin, 2 * d.c, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c, d.c_mid, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c_mid, d.c, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {3 * d.c, d.cout, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0}};
+      *bytes = px * (d.cin + d.cout) * 2;
+      for (const fce_conv_desc& c : cs) *bytes += double(conv_weight_bytes(c));
+      *flops = 2.0 * px * (d.cin * 2.0 * d.c + 9.0 * d.c * d.c_mid + 9.0 * d.c_mid * d.c + 3.0 * d.c * d.cout);
       break;
     }
     case OP_PSA: {
@@ -690,6 +720,22 @@ int fce_net_add_psa_attention(fce_net* net, int qkv, int heads, int kd, int hd, 
   op.head_dim = hd;
   op.pe_w = pe_w;
   op.pe_b = pe_b;
+  op.out = out;
+  op.out_coff = out_coff;
+  net->drop_graph();
+  net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_c3k2(fce_net* net, const fce_c3k2_desc* d, int in, int in_coff, int out, int out_coff) {
+  FCE_CHECK(net && d && valid_buf(net, in, false) && valid_buf(net, out, false), "fce_net_add_c3k2: bad argument");
+  FCE_CHECK(c3k2_fused_ok(*d), "fce_net_add_c3k2: unsupported channel configuration");
+  OpDesc op;
+  op.kind = OP_C3K2;
+  op.c3k2 = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->cin;
   op.out = out;
   op.out_coff = out_coff;
   net->drop_graph();

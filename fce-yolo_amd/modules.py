@@ -341,13 +341,48 @@ class C3k(C3):
 
 
 class C3k2(C2f):
-    """block.py:1064-1084."""
+    """block.py:1064-1084.  With c3k = False and one Bottleneck repeat (the n / s scales' C3k2 at
+    160^2 .. 40^2) the whole block can run as ONE fused kernel (csrc/fused.hip: x read once, the
+    intermediates in LDS, bitwise equal to the four convs).  Opt-in with FCE_FUSE_C3K2=1: measured
+    on MI355X it is still slower than the four tuned convs ("Fused C3k2")."""
 
     def __init__(self, c1, c2, n=1, c3k=False, e=0.5, g=1, shortcut=True):
         super().__init__(c1, c2, n, shortcut, g, e)
         self.m = nn.ModuleList(
             C3k(self.c, self.c, 2, shortcut, g) if c3k else Bottleneck(self.c, self.c, shortcut, g) for _ in range(n)
         )
+
+    def _fused_desc(self, be, x):
+        import os
+
+        if be.shape_only or os.environ.get("FCE_FUSE_C3K2", "0") == "0" or not hasattr(be, "c3k2"):
+            return None
+        if len(self.m) != 1 or type(self.m[0]) is not Bottleneck or not self.m[0].add:
+            return None
+        if x.up or x.layout != N.NHWC or x.dtype != N.F16:
+            return None
+        bt = self.m[0]
+        convs = (self.cv1, bt.cv1, bt.cv2, self.cv2)
+        for cv, k in zip(convs, (1, 3, 3, 1)):
+            c = cv.conv
+            if (c.kernel_size[0] != k or c.stride[0] != 1 or c.groups != 1 or not isinstance(cv.act, nn.SiLU)):
+                return None
+        d = N.C3k2Desc()
+        d.cin, d.c, d.c_mid, d.cout = self.cv1.conv.in_channels, self.c, bt.cv1.conv.out_channels, self.cv2.conv.out_channels
+        if bt.cv1.conv.in_channels != self.c or bt.cv2.conv.out_channels != self.c:
+            return None
+        for i, cv in enumerate(convs):
+            nat = conv_native(cv.conv, getattr(cv, "bn", None), True, be.device)
+            d.w[i], d.b[i] = nat.w.data_ptr(), nat.b.data_ptr()
+        return d if N.lib().fce_c3k2_supported(C.byref(d)) else None
+
+    def emit(self, be, x, out=None):
+        d = self._fused_desc(be, x)
+        if d is None:
+            return super().emit(be, x, out)
+        y = out if out is not None else be.alloc(x.n, self.cv2.conv.out_channels, x.h, x.w)
+        be.c3k2(d, x, y)
+        return y
 
 
 class SPPF(nn.Module):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 2
+#define FCE_ABI_VERSION 3
 
 /* status codes */
 #define FCE_OK 0
@@ -186,6 +186,21 @@ int fce_psa_attention(const fce_tensor* qkv, int heads, int key_dim, int head_di
 int fce_detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
                       float* out, void* stream);
 
+/* ---------------------------------------------------------------- fused blocks */
+/* C3k2 with c3k = False and one Bottleneck repeat (block.py:1064-1084, C2f.forward :303-307,
+ * Bottleneck.forward :474-476): y = SiLU(cv2([a | b | m])), [a | b] = SiLU(cv1(x)),
+ * m = SiLU(m.cv2(SiLU(m.cv1(b)))) + b, in one kernel (t / h / m stay in LDS).  w / b: the four convs'
+ * packed weights (fce_conv_pack_weights) and BN-folded biases, in the order cv1 (cin -> 2c, 1x1),
+ * m.cv1 (c -> c_mid, 3x3), m.cv2 (c_mid -> c, 3x3), cv2 (3c -> cout, 1x1); all SiLU.  Bitwise equal
+ * to the four fce_conv2d calls.  fce_c3k2_supported: channel limits (c, c_mid, cout <= 128, ...). */
+typedef struct fce_c3k2_desc {
+  int cin, c, c_mid, cout;
+  const void* w[4];
+  const float* b[4];
+} fce_c3k2_desc;
+int fce_c3k2_supported(const fce_c3k2_desc* d);
+int fce_c3k2(const fce_c3k2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
+
 /* ---------------------------------------------------------------- NMS */
 size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 /* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
@@ -220,6 +235,7 @@ int fce_net_add_coord(fce_net* net, int kind /*0 BiCoord,1 CoordAtt,2 CoordCross
                       int in_buf, int in_coff, int out_buf, int out_coff);
 int fce_net_add_psa_attention(fce_net* net, int qkv_buf, int heads, int key_dim, int head_dim, const float* pe_w,
                               const float* pe_b, int out_buf, int out_coff);
+int fce_net_add_c3k2(fce_net* net, const fce_c3k2_desc* d, int in_buf, int in_coff, int out_buf, int out_coff);
 /* map_bufs[i]: f32 buffer of level i holding cat(box 4*reg_max, cls nc) channels (head.py:122) */
 int fce_net_add_detect(fce_net* net, int nl, const int* map_bufs, const float* strides, int reg_max);
 /* Fused Detect tail conv (see fce_conv2d_detect) writing the forward's pred output; `level` orders

@@ -37,13 +37,15 @@ def family(name):
                      ("dwconv", "dwconv3x3"), ("maxpool", "maxpool_chain"), ("weighted_add", "bifpn_weighted_add"),
                      ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"), ("pool_kernel", "bicoordcrossatt"),
                      ("coord_", "bicoordcrossatt"), ("gate_apply", "bicoordcrossatt"), ("nms", "nms"),
-                     ("detect_decode", "detect_decode")):
+                     ("detect_decode", "detect_decode"), ("c3k2_fused", "c3k2_fused")):
         if key in name:
             return fam
     return None
 
 
-def profile_dispatches(d, counter):
+def profile_dispatches(d, counter, scale=1024.0):
+    """(dispatch id, kernel, value * scale) of `counter` for the dispatches of bench.py's per-op profile
+    pass (between its 3rd and 4th trace markers).  FETCH_SIZE / WRITE_SIZE are in KB (scale 1024)."""
     rows = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -60,17 +62,34 @@ def profile_dispatches(d, counter):
         raise SystemExit(f"{d}: expected >= 3 trace markers, found {len(marks)}")
     lo = marks[2]
     hi = marks[3] if len(marks) > 3 else 1 << 62
-    return [(i, n, v * 1024.0) for i, n, v in rows if lo < i < hi and "spin_kernel" not in n]
+    return [(i, n, v * scale) for i, n, v in rows if lo < i < hi and "spin_kernel" not in n]
 
 
-def main(fetch_dir, write_dir, prof_path):
+def dispatch_ns(d):
+    """Kernel duration (ns) per dispatch id from the kernel trace of a counter pass."""
+    out = {}
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            out[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return out
+
+
+MFMA_F16_PEAK_TFS = 2500.0
+
+
+def main(fetch_dir, write_dir, prof_path, mfma_dir=None):
     prof = json.load(open(prof_path))
     fe = profile_dispatches(fetch_dir, "FETCH_SIZE")
     wr = profile_dispatches(write_dir, "WRITE_SIZE")
+    mm = mb = None
+    if mfma_dir:  # MFMA pass: f16 MFMA ops executed (x 512 flop) and MFMA-busy cycles, with kernel durations
+        mm = profile_dispatches(mfma_dir, "SQ_INSTS_VALU_MFMA_MOPS_F16", 512.0)
+        mb = profile_dispatches(mfma_dir, "SQ_VALU_MFMA_BUSY_CYCLES", 1.0)
+        mns = dispatch_ns(mfma_dir)
     need = sum(int(p[4]) for p in prof)
     if len(fe) < need or len(wr) < need:
         raise SystemExit(f"profile pass has {len(fe)}/{len(wr)} dispatches, ops need {need}")
-    ops, fam = [], defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+    ops, fam = [], defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0])
     k = 0
     for i, (name, alg, _flops, _ms, nl) in enumerate(prof):
         nl = int(nl)
@@ -78,21 +97,44 @@ def main(fetch_dir, write_dir, prof_path):
         wb = sum(v for _, _, v in wr[k:k + nl])
         kernels = [n.split("(")[0] for _, n, _ in fe[k:k + nl]]
         k += nl
-        ops.append({"op": i, "family": name, "kernels": kernels, "algorithmic_bytes": alg, "fetch_bytes": fb,
-                    "write_bytes": wb, "hbm_bytes": fb + wb, "hbm_over_alg": round((fb + wb) / max(alg, 1.0), 3)})
+        op = {"op": i, "family": name, "kernels": kernels, "algorithmic_bytes": alg, "fetch_bytes": fb,
+              "write_bytes": wb, "hbm_bytes": fb + wb, "hbm_over_alg": round((fb + wb) / max(alg, 1.0), 3)}
         f = fam[name]
+        if mm is not None:
+            j0 = k - nl
+            mflop = sum(v for _, _, v in mm[j0:k])
+            busy = sum(v for _, _, v in mb[j0:k])
+            ns = sum(mns.get(d, 0) for d, _, _ in mm[j0:k])
+            op.update({"mfma_flops": mflop, "mfma_busy_cycles": busy, "counter_pass_ns": ns,
+                       "mfma_tflops": round(mflop / max(ns, 1) / 1e3, 2),
+                       "mfma_frac": round(mflop / max(ns, 1) / 1e3 / MFMA_F16_PEAK_TFS, 4),
+                       "algorithmic_flops": _flops})
+            f[4] += mflop
+            f[5] += ns
+            f[6] += busy
+        ops.append(op)
         f[0] += nl
         f[1] += fb
         f[2] += wb
         f[3] += alg
-    out = {name: {"launches": v[0], "fetch_bytes": v[1] / v[0], "write_bytes": v[2] / v[0],
-                  "hbm_bytes": (v[1] + v[2]) / v[0], "algorithmic_bytes": v[3] / v[0],
-                  "hbm_over_alg": round((v[1] + v[2]) / max(v[3], 1.0), 3)} for name, v in fam.items() if v[0]}
+    out = {}
+    for name, v in fam.items():
+        if not v[0]:
+            continue
+        out[name] = {"launches": v[0], "fetch_bytes": v[1] / v[0], "write_bytes": v[2] / v[0],
+                     "hbm_bytes": (v[1] + v[2]) / v[0], "algorithmic_bytes": v[3] / v[0],
+                     "hbm_over_alg": round((v[1] + v[2]) / max(v[3], 1.0), 3)}
+        if mm is not None and v[5]:
+            out[name].update({"mfma_flops": v[4] / v[0], "mfma_busy_cycles": v[6] / v[0],
+                              "counter_pass_ns": v[5] / v[0], "mfma_tflops": round(v[4] / v[5] / 1e3, 2),
+                              "mfma_frac": round(v[4] / v[5] / 1e3 / MFMA_F16_PEAK_TFS, 4)})
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace), the per-op "
                          "profile pass of one bench.py forward; fetch doubled (gfx950 16-B/lane read correction); "
-                         "family values are per launch (averages)",
+                         "MFMA pass (when present): SQ_INSTS_VALU_MFMA_MOPS_F16 x 512 = f16 MFMA flop executed "
+                         "(padding included), SQ_VALU_MFMA_BUSY_CYCLES, over the kernel durations of that pass "
+                         "(profiled clocks run lower than unprofiled ones); family values are per launch (averages)",
                "families": out, "ops": ops}, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3])
+    main(*sys.argv[1:5])

@@ -220,6 +220,34 @@ def test_full_size_op_parity(key, full_fx, device):
     assert err <= OP_TOL and e_slice <= OP_TOL and e_sum <= OP_TOL, (err, e_slice, e_sum)
 
 
+@pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11s-bifpn.yaml", 2, 256),
+                                             ("yolo11n-fce.yaml", 1, 224)])
+def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, device, monkeypatch):
+    """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give
+    (partial edge tiles at 224: 56 = 3.5 x 16), whole-graph and per-module."""
+    model = cases.seeded_model(cfg, 0).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(9)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_C3K2", "1")
+    eng = Engine(model, batch, imgsz, device)
+    names = [eng.op_info(i)[0] for i in range(eng.num_ops())]
+    assert "c3k2_fused" in names
+    yf = eng(x).clone()
+    monkeypatch.delenv("FCE_FUSE_C3K2")
+    eng2 = Engine(model, batch, imgsz, device)
+    assert "c3k2_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
+    yu = eng2(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(yf, yu)
+    c3 = next(m for m in model.model if isinstance(m, M.C3k2) and not isinstance(m.m[0], M.C3k))
+    xi = torch.randn(batch, c3.cv1.conv.in_channels, 48, 40, device=device).half().contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        u = c3(xi)
+        monkeypatch.setenv("FCE_FUSE_C3K2", "1")
+        f = c3(xi)
+    assert torch.equal(u, f)
+
+
 def test_batch_invariance_640(device):
     """Size-independent property at the bench size: an image's detections do not depend on its batch."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
