@@ -1261,15 +1261,33 @@ __device__ __forceinline__ int tile_slot(int u, int q) {
   return KP == 1 ? (q ^ ((u >> 1) & 3)) : (q ^ (u & 6));
 }
 
-template <int S, int RC, int RP, int CW, int KP>
+// AL = true: the block's weight fragments (CW * RC cout tiles x 9 taps x KP chunks, 1 KiB each) are
+// staged in LDS next to the input tile, once per block per chunk group, and every wave reads its A
+// fragments with ds_read_b128 (conflict-free: lane order).  Without it each wave streams its own A
+// fragments from L2 for every K-step, and at the m/l scales (rc * rp MFMAs per fragment load) the
+// per-CU vector-memory path, not the MFMA, sets the rate.  Same K order: bitwise identical.
+template <int S, int RC, int RP, int CW, int KP, bool AL>
+struct Tile3Geom {
+  static constexpr int TW = 16, RW = 4 / CW, TH = RW * RP;
+  static constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
+  static constexpr int NQ = 4 * KP;
+  static constexpr int NE = RI * CI * NQ, NL = (NE + 255) / 256;
+  static constexpr int NA = AL ? CW * RC * 9 * KP * 64 : 0, NLA = (NA + 255) / 256;
+  static constexpr bool PF = AL ? NL + NLA <= 16 : NL <= 8;  // register prefetch of the next stage
+  static constexpr size_t lds = size_t(PF ? NL * 256 : NE) * 16 + size_t(AL ? (PF ? NLA * 256 : NA) : 0) * 16;
+};
+
+template <int S, int RC, int RP, int CW, int KP, bool AL>
 __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
+  using G = Tile3Geom<S, RC, RP, CW, KP, AL>;
   constexpr int TW = 16, RW = 4 / CW, TH = RW * RP;
   constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;  // staged input rows / cols
   constexpr int NQ = 4 * KP;                                    // 16-byte pieces per staged pixel
-  constexpr int NE0 = RI * CI * NQ, NL0 = (NE0 + 255) / 256;
-  // with the register prefetch (NL0 <= 8) the image is padded to NL0 * 256 pieces so that the last
-  // staging round stores unconditionally (see conv3x3_ring_kernel)
-  __shared__ __attribute__((aligned(16))) h8 tile[NL0 <= 8 ? NL0 * 256 : NE0];
+  constexpr int NL0 = G::NL;
+  // with the register prefetch the image is padded to NL0 * 256 pieces so that the last staging round
+  // stores unconditionally (see conv3x3_ring_kernel)
+  __shared__ __attribute__((aligned(16))) h8 tile[G::PF ? NL0 * 256 : G::NE];
+  __shared__ __attribute__((aligned(16))) h8 atile[AL ? (G::PF ? G::NLA * 256 : G::NA) : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int wc = wave / RW, wr = wave - wc * RW;
@@ -1296,15 +1314,28 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
   h8 af[RC];  // A fragments of the current K-step (prefetched one step ahead in the tap loop)
+  if constexpr (!AL) {
 #pragma unroll
-  for (int r = 0; r < RC; ++r) af[r] = wfrag[r][0];
+    for (int r = 0; r < RC; ++r) af[r] = wfrag[r][0];
+  }
   const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   // Staging: NL pieces per thread.  When they fit in registers (NL <= 8) the next stage's global
   // loads are issued right after this stage's LDS image is complete, so they are in flight during
   // this stage's MFMAs (register double buffer; one LDS image).
-  constexpr int NE = RI * CI * NQ, NL = (NE + 255) / 256;
-  constexpr bool PF = NL <= 8;
+  constexpr int NE = G::NE, NL = G::NL, NA = G::NA, NLA = G::NLA;
+  constexpr bool PF = G::PF;
+  // A piece e of chunk group c0: fragment f = (block cout tile, k, tap) in that order, lane e & 63
+  const h8* wblk = reinterpret_cast<const h8*>(a.w);
+  const int ct_blk = cog * CW * RC;
+  auto apiece = [&](int e, int c0) -> h8 {
+    const int f = e >> 6, l = e & 63;
+    const int rb = f / (9 * KP), rem = f - rb * (9 * KP);
+    const int ct = min(ct_blk + rb, cotiles - 1);
+    // select the address, not the loaded value: a select of two h8 values is done per 16-bit half and
+    // makes the prefetch wait for its own loads right after issuing them
+    return *(e < NA ? wblk + (size_t(ct) * a.nalloc + c0 * 9 + rem) * 64 + l : reinterpret_cast<const h8*>(g_zero_line));
+  };
   auto piece = [&](int e, int c0, int& u, int& slot) -> h8 {
     const int pc = e / NQ, q = e - pc * NQ;
     const int r = pc / CI, c = pc - r * CI;
@@ -1317,11 +1348,16 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
   };
   h8 pv[PF ? NL : 1];
   int ps[PF ? NL : 1];
+  h8 pa[PF && AL ? NLA : 1];
   if constexpr (PF) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       int u;
       pv[i] = piece(threadIdx.x + 256 * i, 0, u, ps[i]);
+    }
+    if constexpr (AL) {
+#pragma unroll
+      for (int i = 0; i < NLA; ++i) pa[i] = apiece(threadIdx.x + 256 * i, 0);
     }
   }
   for (int c0 = 0; c0 < spt; c0 += KP) {
@@ -1329,12 +1365,18 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
     if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < NL; ++i) tile[ps[i]] = pv[i];
+      if constexpr (AL) {
+#pragma unroll
+        for (int i = 0; i < NLA; ++i) atile[threadIdx.x + 256 * i] = pa[i];
+      }
     } else {
       for (int e = threadIdx.x; e < NE; e += 256) {
         int u, sl;
         const h8 v = piece(e, c0, u, sl);
         tile[sl] = v;
       }
+      if constexpr (AL)
+        for (int e = threadIdx.x; e < NA; e += 256) atile[e] = apiece(e, c0);
     }
     __syncthreads();
     if constexpr (PF) {
@@ -1343,6 +1385,10 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
         for (int i = 0; i < NL; ++i) {
           int u;
           pv[i] = piece(threadIdx.x + 256 * i, c0 + KP, u, ps[i]);
+        }
+        if constexpr (AL) {
+#pragma unroll
+          for (int i = 0; i < NLA; ++i) pa[i] = apiece(threadIdx.x + 256 * i, c0 + KP);
         }
       }
     }
@@ -1358,8 +1404,13 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
         const int ks = (c0 + k) * 9 + tap + 1;
         const int ksn = ks < spt * 9 ? ks : ks - 1;
         h8 an[RC];
+        if constexpr (AL) {
 #pragma unroll
-        for (int r = 0; r < RC; ++r) an[r] = wfrag[r][ksn * 64];
+          for (int r = 0; r < RC; ++r) af[r] = atile[(((wc * RC + r) * KP + k) * 9 + tap) * 64 + lane];
+        } else {
+#pragma unroll
+          for (int r = 0; r < RC; ++r) an[r] = wfrag[r][ksn * 64];
+        }
 #pragma unroll
         for (int p = 0; p < RP; ++p) {
           const int ry = (wr * RP + p) * S + ky;
@@ -1371,8 +1422,10 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 #pragma unroll
           for (int p = 0; p < RP; ++p)
             acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
+        if constexpr (!AL) {
 #pragma unroll
-        for (int r = 0; r < RC; ++r) af[r] = an[r];
+          for (int r = 0; r < RC; ++r) af[r] = an[r];
+        }
       }
     }
   }
@@ -2369,9 +2422,16 @@ static void launch_dense_rc(const ConvArgs& a, int out_kind, bool fast, int rc, 
     launch_dense_rp<KS, 4>(a, out_kind, fast, rc, s);
 }
 
-// Tile-kernel configurations, coded 0x100 | rc | rp << 4 | log2(cw) << 12 | (kp - 1) << 14
+// Tile-kernel configurations, coded 0x100 | rc | rp << 4 | log2(cw) << 12 | (kp - 1) << 14 | al << 15
 static constexpr size_t tile3_lds(int s, int rp, int cw, int kp) {
   return size_t(((4 / cw) * rp - 1) * s + 3) * (15 * s + 3) * 4 * kp * 16;
+}
+// A-in-LDS variants: rc 2 / 4, rc * rp <= 16 (registers: the accumulators plus up to 16 staged pieces
+// per thread), input tile + weight stage within 96 KiB
+static constexpr bool tile3al_ok(int s, int rc, int rp, int cw, int kp) {
+  return (rc == 2 || rc == 4) && (rp == 2 || rp == 4 || rp == 8) && (cw == 1 || cw == 2 || cw == 4) &&
+         (kp == 1 || kp == 2) && rc * rp <= 16 &&
+         tile3_lds(s, rp, cw, kp) + size_t(cw) * rc * 9 * kp * 1024 <= 96 * 1024;
 }
 // rp = 8 (8 output rows per wave: every A fragment read from L2 feeds 8 MFMAs, the m/l-scale 3x3 convs
 // are L2-bound at rp <= 4) only with rc >= 2 and the couts split over 2 / 4 waves
@@ -2385,6 +2445,13 @@ static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
 // encoded 100 + variant (the executor times them at plan time and keeps the fastest; neither
 // changes the per-output summation order, so results are bitwise the same for every choice).
 // Returns the count; 0 for the stem.
+static bool no_tile3al() {  // diagnostics: FCE_NO_TILE3AL=1 drops the A-in-LDS 3x3 variants
+  static const bool v = [] {
+    const char* e = getenv("FCE_NO_TILE3AL");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
 static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (ring) variants
   static const bool v = [] {
     const char* e = getenv("FCE_NO_RING");
@@ -2459,49 +2526,69 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
               out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14);
         }
     }
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 128 && !no_tile3al())  // A in LDS: | 1 << 15
+    for (int kp : {1, 2}) {
+      if (kp == 2 && d.cin % 64 != 0) continue;
+      for (int cwl = 0; cwl < 3; ++cwl)
+        for (int rc : {2, 4}) {
+          const int cb = (1 << cwl) * rc;
+          if ((cb >> 1) >= cotiles) continue;
+          for (int rp : {2, 4, 8})
+            if (n < cap && tile3al_ok(d.stride, rc, rp, 1 << cwl, kp))
+              out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14) | (1 << 15);
+        }
+    }
   return n;
 }
 
 template <int S, int RC, int RP, int CW, int KP>
-static void launch_tile3_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if constexpr (tile3_lds(S, RP, CW, KP) <= 80 * 1024)
-    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, RP, CW, KP>), grid, dim3(256), 0, s, a);
+static void launch_tile3_k(const ConvArgs& a, bool al, dim3 grid, hipStream_t s) {
+  if (al) {
+    if constexpr (tile3al_ok(S, RC, RP, CW, KP)) {
+      static_assert(Tile3Geom<S, RC, RP, CW, KP, true>::lds <= 160 * 1024, "A-in-LDS tile too large");
+      FCE_LAUNCH((conv3x3_tile_kernel<S, RC, RP, CW, KP, true>), grid, dim3(256), 0, s, a);
+    }
+  } else if constexpr (tile3_lds(S, RP, CW, KP) <= 80 * 1024) {
+    FCE_LAUNCH((conv3x3_tile_kernel<S, RC, RP, CW, KP, false>), grid, dim3(256), 0, s, a);
+  }
 }
 
 template <int S, int RC, int RP>
-static void launch_tile3_w(const ConvArgs& a, int cw, int kp, dim3 grid, hipStream_t s) {
+static void launch_tile3_w(const ConvArgs& a, int cw, int kp, bool al, dim3 grid, hipStream_t s) {
   if (cw == 1)
-    kp == 1 ? launch_tile3_k<S, RC, RP, 1, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 1, 2>(a, grid, s);
+    kp == 1 ? launch_tile3_k<S, RC, RP, 1, 1>(a, al, grid, s) : launch_tile3_k<S, RC, RP, 1, 2>(a, al, grid, s);
   else if (cw == 2)
-    kp == 1 ? launch_tile3_k<S, RC, RP, 2, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 2, 2>(a, grid, s);
+    kp == 1 ? launch_tile3_k<S, RC, RP, 2, 1>(a, al, grid, s) : launch_tile3_k<S, RC, RP, 2, 2>(a, al, grid, s);
   else
-    kp == 1 ? launch_tile3_k<S, RC, RP, 4, 1>(a, grid, s) : launch_tile3_k<S, RC, RP, 4, 2>(a, grid, s);
+    kp == 1 ? launch_tile3_k<S, RC, RP, 4, 1>(a, al, grid, s) : launch_tile3_k<S, RC, RP, 4, 2>(a, al, grid, s);
 }
 
 template <int S, int RC>
-static void launch_tile3_rc(const ConvArgs& a, int rp, int cw, int kp, dim3 grid, hipStream_t s) {
+static void launch_tile3_rc(const ConvArgs& a, int rp, int cw, int kp, bool al, dim3 grid, hipStream_t s) {
   if (rp == 1)
-    launch_tile3_w<S, RC, 1>(a, cw, kp, grid, s);
+    launch_tile3_w<S, RC, 1>(a, cw, kp, al, grid, s);
   else if (rp == 2)
-    launch_tile3_w<S, RC, 2>(a, cw, kp, grid, s);
+    launch_tile3_w<S, RC, 2>(a, cw, kp, al, grid, s);
   else if (rp == 4)
-    launch_tile3_w<S, RC, 4>(a, cw, kp, grid, s);
-  else if constexpr (RC >= 2) {  // rp == 8: cw 2 / 4 only (tile3_ok)
-    if (cw == 2)
-      kp == 1 ? launch_tile3_k<S, RC, 8, 2, 1>(a, grid, s) : launch_tile3_k<S, RC, 8, 2, 2>(a, grid, s);
+    launch_tile3_w<S, RC, 4>(a, cw, kp, al, grid, s);
+  else if constexpr (RC >= 2) {  // rp == 8: cw 2 / 4 (tile3_ok), any cw with A in LDS (tile3al_ok)
+    if (cw == 1)
+      kp == 1 ? launch_tile3_k<S, RC, 8, 1, 1>(a, al, grid, s) : launch_tile3_k<S, RC, 8, 1, 2>(a, al, grid, s);
+    else if (cw == 2)
+      kp == 1 ? launch_tile3_k<S, RC, 8, 2, 1>(a, al, grid, s) : launch_tile3_k<S, RC, 8, 2, 2>(a, al, grid, s);
     else
-      kp == 1 ? launch_tile3_k<S, RC, 8, 4, 1>(a, grid, s) : launch_tile3_k<S, RC, 8, 4, 2>(a, grid, s);
+      kp == 1 ? launch_tile3_k<S, RC, 8, 4, 1>(a, al, grid, s) : launch_tile3_k<S, RC, 8, 4, 2>(a, al, grid, s);
   }
 }
 
 template <int S>
-static void launch_tile3_s(const ConvArgs& a, int rc, int rp, int cw, int kp, dim3 grid, hipStream_t s) {
+static void launch_tile3_s(const ConvArgs& a, int rc, int rp, int cw, int kp, bool al, dim3 grid, hipStream_t s) {
   if (rc == 1)
-    launch_tile3_rc<S, 1>(a, rp, cw, kp, grid, s);
+    launch_tile3_rc<S, 1>(a, rp, cw, kp, al, grid, s);
   else if (rc == 2)
-    launch_tile3_rc<S, 2>(a, rp, cw, kp, grid, s);
+    launch_tile3_rc<S, 2>(a, rp, cw, kp, al, grid, s);
   else
-    launch_tile3_rc<S, 4>(a, rp, cw, kp, grid, s);
+    launch_tile3_rc<S, 4>(a, rp, cw, kp, al, grid, s);
 }
 
 template <int S, int RC>
@@ -2541,8 +2628,8 @@ static int launch_small3(const ConvArgs& a, int rc, int rp, int stride, int n, h
   return launch_status("conv3x3_tile_small_kernel");
 }
 
-static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, int stride, int n, hipStream_t s) {
-  FCE_CHECK(tile3_ok(stride, rc, rp, cw, kp), "conv 3x3 tile: bad configuration");
+static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, bool al, int stride, int n, hipStream_t s) {
+  FCE_CHECK(al ? tile3al_ok(stride, rc, rp, cw, kp) : tile3_ok(stride, rc, rp, cw, kp), "conv 3x3 tile: bad configuration");
   const int th = (4 / cw) * rp;
   const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
   FCE_CHECK(tiles < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
@@ -2551,9 +2638,9 @@ static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, int s
   FCE_CHECK(tiles * b.gy < (int64_t(1) << 31), "conv 3x3 tile: grid too large");
   const dim3 grid(unsigned(tiles * b.gy));
   if (stride == 1)
-    launch_tile3_s<1>(b, rc, rp, cw, kp, grid, s);
+    launch_tile3_s<1>(b, rc, rp, cw, kp, al, grid, s);
   else
-    launch_tile3_s<2>(b, rc, rp, cw, kp, grid, s);
+    launch_tile3_s<2>(b, rc, rp, cw, kp, al, grid, s);
   return launch_status("conv3x3_tile_kernel");
 }
 
@@ -2829,10 +2916,12 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     rc = tile & 15;
     rp = (tile >> 4) & 15;
     const int cw = 1 << ((tile >> 12) & 3), kp = ((tile >> 14) & 1) + 1;
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && tile3_ok(d.stride, rc, rp, cw, kp) &&
+    const bool al = (tile >> 15) & 1;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 &&
+                  (al ? tile3al_ok(d.stride, rc, rp, cw, kp) : tile3_ok(d.stride, rc, rp, cw, kp)) &&
                   (kp == 1 || d.cin % 64 == 0),
               "conv: bad LDS-tile hint");
-    return launch_tile3(a, rc, rp, cw, kp, d.stride, x.n, s);
+    return launch_tile3(a, rc, rp, cw, kp, al, d.stride, x.n, s);
   }
   FCE_CHECK(kind <= 0, "conv: unknown kernel variant");
   if (tile >= 0) {

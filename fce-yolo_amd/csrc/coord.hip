@@ -440,6 +440,7 @@ struct CoreArgs {
   const float* bo[2];
   float* g[2];         // [N][L][oup] gate logits
   int H, W, C, mid, heads, oup;
+  int qsplit;  // query chunks per (image, branch): blockIdx.z takes rows [z * qc, z * qc + qc) of the queries
   float scale;
   unsigned long long* tm;  // diagnostics (FCE_COORD_TIMING): per-workgroup phase clocks, else null
 };
@@ -460,8 +461,12 @@ __global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
   // row strides: lc = C + 4 floats (16-byte rows; a wave's 16 positions land on distinct bank quads),
   // lm = mid + 4
   const int C = a.C, mid = a.mid, oup = a.oup, lc = C + 4, lm = mid + 4;
-  const int Lq = br == 0 ? a.H : a.W, Lk = br == 0 ? a.W : a.H;
-  const float* gq = (br == 0 ? a.xh + int64_t(n) * a.H * C : a.xw + int64_t(n) * a.W * C);
+  const int Lq0 = br == 0 ? a.H : a.W, Lk = br == 0 ? a.W : a.H;
+  // query chunk of this workgroup: every chunk projects all keys / values (cheap at these sizes) and
+  // only its own queries, so the attention and the output projection spread over qsplit CUs
+  const int qc = (Lq0 + a.qsplit - 1) / a.qsplit, q0 = min(Lq0, int(blockIdx.z) * qc);
+  const int Lq = min(Lq0, q0 + qc) - q0;
+  const float* gq = (br == 0 ? a.xh + int64_t(n) * a.H * C : a.xw + int64_t(n) * a.W * C) + int64_t(q0) * C;
   const float* gk = (br == 0 ? a.xw + int64_t(n) * a.W * C : a.xh + int64_t(n) * a.H * C);
   const int L = a.H > a.W ? a.H : a.W;
   float* wq = sm;                // [C][mid]
@@ -600,7 +605,7 @@ __global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
   __syncthreads();
   unsigned long long t3 = a.tm ? __builtin_amdgcn_s_memtime() : 0;
   // output projection to the gate logits, task = (position, 4 consecutive outputs), 16-byte stores
-  float* g = a.g[br] + int64_t(n) * Lq * oup;
+  float* g = a.g[br] + (int64_t(n) * Lq0 + q0) * oup;
   const float* bo = a.bo[br];
   const int o4n = oup / 4;
   for (int e = threadIdx.x; e < Lq * o4n; e += CORE_THREADS) {
@@ -621,7 +626,7 @@ __global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
     __syncthreads();
     const unsigned long long t4 = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) {
-      unsigned long long* o = a.tm + (blockIdx.y * gridDim.x + blockIdx.x) * 5;
+      unsigned long long* o = a.tm + ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 5;
       o[0] = t0;
       o[1] = t1 - t0;
       o[2] = t2 - t1;
@@ -783,12 +788,22 @@ static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, 
   a.heads = d.heads;
   a.oup = d.oup;
   a.scale = d.scale;
+  // query chunks: enough workgroups to cover the CUs (2 N (image, branch) pairs alone leave most idle),
+  // at least 8 queries per chunk
+  {
+    const int L = H < W ? H : W;
+    int qs = 1;
+    while (qs < 8 && 2 * N * qs < 256 && L / (2 * qs) >= 8) qs *= 2;
+    const char* qe = getenv("FCE_COORD_QSPLIT");  // diagnostics: force the query split
+    if (qe && atoi(qe) > 0) qs = atoi(qe);
+    a.qsplit = qs;
+  }
   a.tm = nullptr;
   static unsigned long long* tm_buf = nullptr;
   const char* tenv = getenv("FCE_COORD_TIMING");
   if (tenv && atoi(tenv)) {
     if (!tm_buf) FCE_HIP_CHECK(hipMalloc(&tm_buf, size_t(2) * 4096 * 5 * 8));
-    a.tm = N <= 4096 ? tm_buf : nullptr;
+    a.tm = N * a.qsplit <= 4096 ? tm_buf : nullptr;
   }
   const size_t shm = core_lds_floats(H, W, d.inp, d.mid, d.oup) * sizeof(float);
   switch (d.mid / d.heads) {
@@ -798,7 +813,7 @@ static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, 
                                                     hipFuncAttributeMaxDynamicSharedMemorySize,               \
                                                     160 * 1024) == hipSuccess;                                \
     if (!lds_ok && shm > 64 * 1024) return fail(FCE_ERR_HIP, "coord core: cannot opt in to >64 KiB LDS");     \
-    FCE_LAUNCH(coord_core_kernel<DH>, dim3(N, 2), dim3(CORE_THREADS), shm, s, a);                                      \
+    FCE_LAUNCH(coord_core_kernel<DH>, dim3(N, 2, a.qsplit), dim3(CORE_THREADS), shm, s, a);                            \
     break;                                                                                                    \
   }
     CORE(1) CORE(2) CORE(4) CORE(8) CORE(16)
@@ -808,17 +823,18 @@ static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, 
   }
   int st = launch_status("coord_core_kernel");
   if (!st && a.tm) {  // diagnostics: print the phase clocks of this launch
-    std::vector<unsigned long long> h(size_t(2) * N * 5);
+    const int nb = 2 * N * a.qsplit;
+    std::vector<unsigned long long> h(size_t(nb) * 5);
     FCE_HIP_CHECK(hipStreamSynchronize(s));
     FCE_HIP_CHECK(hipMemcpy(h.data(), a.tm, h.size() * 8, hipMemcpyDeviceToHost));
     unsigned long long mn = ~0ull, mx = 0, ph[4] = {0, 0, 0, 0};
-    for (int b = 0; b < 2 * N; ++b) {
+    for (int b = 0; b < nb; ++b) {
       mn = std::min(mn, h[b * 5]);
       mx = std::max(mx, h[b * 5]);
       for (int k = 0; k < 4; ++k) ph[k] += h[b * 5 + 1 + k];
     }
-    fprintf(stderr, "coord_core N%d H%d W%d: start spread %llu, mean phase clocks stage %llu proj %llu attend %llu out %llu\n",
-            N, H, W, mx - mn, ph[0] / (2 * N), ph[1] / (2 * N), ph[2] / (2 * N), ph[3] / (2 * N));
+    fprintf(stderr, "coord_core N%d H%d W%d qsplit %d: start spread %llu, mean phase clocks stage %llu proj %llu attend %llu out %llu\n",
+            N, H, W, a.qsplit, mx - mn, ph[0] / nb, ph[1] / nb, ph[2] / nb, ph[3] / nb);
   }
   return st;
 }

@@ -443,6 +443,9 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (64, 80, 3, 2, 41, 37, False),
     # wide 1x1s of the m/l scales (big-tile K-pipelined kernel, 0x7xx): odd K-step counts, partial cout tiles
     (512, 256, 1, 1, 40, 40, True), (96, 256, 1, 1, 33, 35, False), (136, 72, 1, 1, 19, 23, True),
+    # m/l 3x3s (A-in-LDS tile kernel, 0x81xx): partial cout groups, odd chunk counts, stride 2, residual
+    (256, 256, 3, 1, 40, 40, True), (128, 80, 3, 2, 41, 37, False), (192, 128, 3, 1, 37, 29, True),
+    (160, 48, 3, 1, 21, 19, False),
 ]
 
 
