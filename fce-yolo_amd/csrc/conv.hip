@@ -2445,12 +2445,10 @@ static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
 // encoded 100 + variant (the executor times them at plan time and keeps the fastest; neither
 // changes the per-output summation order, so results are bitwise the same for every choice).
 // Returns the count; 0 for the stem.
-static bool no_tile3al() {  // diagnostics: FCE_NO_TILE3AL=1 drops the A-in-LDS 3x3 variants
-  static const bool v = [] {
-    const char* e = getenv("FCE_NO_TILE3AL");
-    return e && atoi(e) != 0;
-  }();
-  return v;
+static bool tile3al_on() {  // FCE_TILE3AL=1 adds the A-in-LDS 3x3 variants (they lose on every l / m layer
+                             // measured, so the planner does not spend autotune time on them by default)
+  const char* e = getenv("FCE_TILE3AL");
+  return e && atoi(e) != 0;
 }
 static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (ring) variants
   static const bool v = [] {
@@ -2526,7 +2524,7 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
               out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14);
         }
     }
-  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 128 && !no_tile3al())  // A in LDS: | 1 << 15
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 128 && tile3al_on())  // A in LDS: | 1 << 15
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
       for (int cwl = 0; cwl < 3; ++cwl)

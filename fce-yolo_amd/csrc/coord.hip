@@ -788,12 +788,13 @@ static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, 
   a.heads = d.heads;
   a.oup = d.oup;
   a.scale = d.scale;
-  // query chunks: enough workgroups to cover the CUs (2 N (image, branch) pairs alone leave most idle),
-  // at least 8 queries per chunk
+  // query chunks: 2 N (image, branch) workgroups alone leave most CUs idle; up to 4 chunks of at least
+  // 8 queries.  The split depends on the map size only, never on N: the chunk size sets the attention's
+  // key split, so a batch-dependent split would break batch invariance (test_batch_invariance_640).
   {
     const int L = H < W ? H : W;
     int qs = 1;
-    while (qs < 8 && 2 * N * qs < 256 && L / (2 * qs) >= 8) qs *= 2;
+    while (qs < 4 && L / (2 * qs) >= 8) qs *= 2;
     const char* qe = getenv("FCE_COORD_QSPLIT");  // diagnostics: force the query split
     if (qe && atoi(qe) > 0) qs = atoi(qe);
     a.qsplit = qs;
