@@ -7,9 +7,12 @@
 A step = one global batch of B images per GPU through `dist.ShardedPredictor`: each rank's contiguous
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (direct launches; --graph 1 for hipGraph replay) + the device NMS, and
-with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  The
-NMS + gather of batch i run on a side stream under the forward of batch i+1 (engine.Pipeline);
---sequential runs forward and NMS back to back.  Weights are the portable seeded weights of the named
+with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
+default three batches are in flight per GPU (--lanes 3, engine.Pipeline lanes): three executors with their
+own arenas on three streams, each running forward then NMS of every third batch, so one batch's
+latency-bound coarse layers and NMS share the CUs with the next batch's full-width layers; the gather
+runs on a side stream in batch order.  --lanes 1 keeps one executor (the NMS of batch i on a side stream
+under the forward of batch i+1); --sequential runs forward and NMS back to back.  Weights are the portable seeded weights of the named
 architecture (no checkpoints offline), broadcast from rank 0 over RCCL.  Per-GPU work is fixed as N
 grows: scaling is weak.  Prints ONE JSON line on rank 0.
 """
@@ -74,6 +77,8 @@ def parse_args():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
     ap.add_argument("--sequential", action="store_true", help="forward then NMS on one stream (no overlap)")
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FCE_LANES", "3")),
+                    help="batches in flight per GPU (engine.Pipeline lanes: one executor + stream each)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay a captured hipGraph; 0: direct launches "
                     "(measured faster on ROCm 7.2, DESIGN.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
@@ -189,9 +194,11 @@ def main():
 
     B, S = a.batch, a.imgsz
     # this rank's contiguous shard of a global batch of B * world images (dist.ShardedPredictor)
-    sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")))
+    sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")),
+                          lanes=a.lanes)
     eng = sp.engine
-    eng.graph = bool(a.graph)
+    for e in sp.pipe.engs:
+        e.graph = bool(a.graph)
     x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
     nms = NMS(B, eng.anchors, eng.nc, dev)
 
@@ -299,7 +306,8 @@ def main():
         "dtype": "fp16",
         "data": "synthetic torch.rand(B,3,S,S) fp16 per rank; seeded random-init weights of the architecture",
         "config": {"workload": f"{stem} detection inference (forward + decode + NMS) @ {S}x{S}, {B} images/GPU",
-                   "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}"},
+                   "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}",
+                   "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes},
         "roofline": roof,
         "forward_ms_per_batch": round(fwd_ms, 4),
         "forward_kernel_busy_ms": round(kernel_ms, 4),

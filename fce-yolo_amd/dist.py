@@ -122,7 +122,8 @@ class ShardedPredictor:
     stream (``dist.all_gather_into_tensor``; RCCL over xGMI on the GPU box), so the gather of batch i
     overlaps the forward of batch i+1.  `results(k)` unpacks slot k in the unsharded image order."""
 
-    def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, depth: int = 2, **nms_kw):
+    def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, depth: int = 2,
+                 lanes: int = 1, **nms_kw):
         from .engine import NMS, Engine, Pipeline
 
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -136,13 +137,15 @@ class ShardedPredictor:
         self.bmax = max(self.sizes)
         self.engine = Engine(model, self.batch, imgsz, device)
         self.max_det = nms_kw.get("max_det", 300)
+        lanes = max(1, int(lanes))
+        depth = -(-max(depth, lanes) // lanes) * lanes  # Pipeline's slot count
         nb = NMS.packed_bytes(self.bmax, self.max_det)
         # each rank's packed outputs padded to bmax images, so every rank contributes the same bytes
         self.send = [torch.zeros(nb if self.batch < self.bmax else 0, dtype=torch.uint8, device=device)
                      for _ in range(depth)]
         self.gathered = [torch.zeros(self.world * nb if self.world > 1 else 0, dtype=torch.uint8, device=device)
                          for _ in range(depth)]
-        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.world > 1 else None, **nms_kw)
+        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.world > 1 else None, lanes=lanes, **nms_kw)
 
     def _gather(self, k: int):
         from .engine import NMS
@@ -175,4 +178,6 @@ class ShardedPredictor:
         return unpack_gathered(g, self.sizes, self.max_det)
 
     def close(self):
-        self.engine.close()
+        torch.cuda.synchronize(self.engine.device)
+        for e in self.pipe.engs:
+            e.close()

@@ -393,11 +393,12 @@ def test_fused_best_class_keys_match_pred_and_nms(device):
         assert torch.equal(n1.buf, n2.buf)
 
 
-@pytest.mark.parametrize("defer", [True, False])
-def test_pipeline_overlap_matches_sequential(defer, device):
+@pytest.mark.parametrize("defer,lanes", [(True, 1), (False, 1), (False, 2)])
+def test_pipeline_overlap_matches_sequential(defer, lanes, device):
     """engine.Pipeline (forward i+1 overlapping NMS i, double-buffered; deferred to the next forward's
-    fork point or right after the forward) gives every batch exactly the sequential forward + NMS
-    result; so does dist.ShardedPredictor on one rank."""
+    fork point or right after the forward; or two lanes = two executors on two streams with two batches
+    in flight) gives every batch exactly the sequential forward + NMS result; so does
+    dist.ShardedPredictor on one rank."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
     B, S = 4, 320
     eng = Engine(model, B, S, device)
@@ -408,22 +409,22 @@ def test_pipeline_overlap_matches_sequential(defer, device):
         nms(eng(x))
         d, k = nms.results()
         seq.append(([t.clone() for t in d], [t.clone() for t in k]))
-    pipe = Pipeline(eng, depth=2, defer=defer)
+    pipe = Pipeline(eng, depth=2, defer=defer, lanes=lanes)
     got = [pipe.submit(x) for x in xs]  # back to back; only the last `depth` batches remain in their slots
     for i in range(len(xs) - 2, len(xs)):
         d, k = pipe.results(got[i])
         for b in range(B):
             assert torch.equal(d[b], seq[i][0][b]) and torch.equal(k[b], seq[i][1][b]), (i, b)
     # and every batch, by draining after each submit
-    pipe2 = Pipeline(eng, depth=2, defer=defer)
+    pipe2 = Pipeline(eng, depth=2, defer=defer, lanes=lanes)
     for i, x in enumerate(xs):
         d, k = pipe2.results(pipe2.submit(x))
         for b in range(B):
             assert torch.equal(d[b], seq[i][0][b]) and torch.equal(k[b], seq[i][1][b]), (i, b)
-    if defer:
+    if defer or lanes > 1:
         from fce_yolo_amd.dist import ShardedPredictor
 
-        sp = ShardedPredictor(model, B, S, device)
+        sp = ShardedPredictor(model, B, S, device, lanes=lanes)
         slots = [sp.submit(x) for x in xs]
         for i in range(len(xs) - 2, len(xs)):
             d, k = sp.results(slots[i])
