@@ -1439,7 +1439,9 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 // whole launch; the block (4 cout tiles) walks a sequence of TH = RP row x 16 column output tiles,
 // staging each tile's input (+ halo, all cin, 64 * NCH bytes per pixel, the swizzled image of the tile
 // kernels) in one of two LDS buffers while the previous tile computes (the next tile's global loads are
-// issued before this tile's MFMAs).  Block b: XCD b % 8, cout group, slot; tiles xcd + 8 (slot + k nslot).
+// issued before this tile's MFMAs).  Block b: XCD b % 8, cout group, slot; XCD x owns the contiguous tile
+// range [x chunk, (x + 1) chunk) and its slot-th blocks take tiles x chunk + slot + k nslot, so the tiles
+// whose halos overlap are in flight on one XCD's L2 at the same time.
 // K order (chunk, tap) is the implicit-GEMM kernel's: bitwise identical.
 template <int S, int RP, int NCH>
 __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot) {
@@ -1457,8 +1459,9 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
   const int by = loc % a.gy, slot = loc / a.gy;
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   const int ntiles = tiles_x * tiles_y * a.N;
-  int t = xcd + 8 * slot;
-  if (t >= ntiles) return;  // block-uniform
+  const int chunk = (ntiles + 7) >> 3, tend = min(ntiles, (xcd + 1) * chunk);
+  int t = xcd * chunk + slot;
+  if (t >= tend) return;  // block-uniform
   const int cot0 = by * 4 + wave;
   const int cotiles = (a.cout + 15) >> 4;
   h8 af[NCH * 9];
@@ -1487,14 +1490,14 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
   h8 v[NL];
   int sl[NL];
   stage_load(t, v, sl);
-  const int step = 8 * nslot;
-  for (int cur = 0; t < ntiles; cur ^= 1) {
+  const int step = nslot;
+  for (int cur = 0; t < tend; cur ^= 1) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) tile[cur * BUF + sl[i]] = v[i];
     __syncthreads();
     const int tn = t + step;
     const int tx = t % tiles_x, r0 = t / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
-    if (tn < ntiles) stage_load(tn, v, sl);
+    if (tn < tend) stage_load(tn, v, sl);
     f4 acc[1][RP];
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[0][p] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1843,14 +1846,26 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
 // lines); each thread computes PY outputs down its column from (PY-1)*S+3 input rows, every loaded
 // row feeding all the outputs that use it.  Out-of-image taps are skipped (selects, no branches) and
 // each output accumulates its taps in (ky, kx) order with fmaf, like the other variants.
+// XCD-aware 2-D block order: block b runs on XCD b % 8; logical block L = (b % 8) * per + b / 8 gives each
+// XCD a contiguous run of (x fastest, then y) blocks, so the row bands that share halo rows meet in one L2
+__device__ __forceinline__ void xcd_block2(int& bx, int& by) {
+  const int gx = int(gridDim.x), total = gx * int(gridDim.y), b = int(blockIdx.y) * gx + int(blockIdx.x);
+  const int per = total >> 3, body = per << 3;
+  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+  by = L / gx;
+  bx = L - by * gx;
+}
+
 template <int S, int PY>
 __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
   const int cg = a.C >> 3;
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  int bx, by;
+  xcd_block2(bx, by);
+  const int e = bx * 256 + threadIdx.x;
   if (e >= a.Wo * cg) return;
   const int ox = e / cg, g = e - ox * cg, c0 = g * 8;
   const int bands = (a.Ho + PY - 1) / PY;
-  const int n = blockIdx.y / bands, oy0 = (blockIdx.y - n * bands) * PY;
+  const int n = by / bands, oy0 = (by - n * bands) * PY;
   float wk[9][8], acc[PY][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
