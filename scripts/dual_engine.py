@@ -23,8 +23,10 @@ model = DetectionModel(cfg)
 model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
 model.eval().to(dev)
 xs = [torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(i)).half().to(dev) for i in range(2)]
-engs = [Engine(model, B, S, dev), Engine(model, B, S, dev)]
-streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+NL = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+engs = [Engine(model, B, S, dev)]
+engs += [engs[0].clone() for _ in range(NL - 1)]
+streams = [torch.cuda.Stream(dev) for _ in range(NL)]
 ref = [engs[0](xs[i]).clone() for i in range(2)]
 torch.cuda.synchronize()  # the side streams below do not order against the null stream
 K = 40
@@ -45,10 +47,10 @@ def run(n_eng):
     return (time.perf_counter() - t0) / K * 1e3
 
 
-for n in (1, 2, 1, 2):
+for n in list(range(1, NL + 1)) * 2:
     print(f"engines {n}: {run(n):.4f} ms per batch", flush=True)
 bad = 0
-for k in range(2):
+for k in range(NL):
     for j in range(2):
         with torch.cuda.stream(streams[k]):
             y = engs[k](xs[j]).clone()
