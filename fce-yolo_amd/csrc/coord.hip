@@ -569,27 +569,60 @@ __global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
       acc[d] = 0.f;
     }
     float m = -INFINITY;
-#pragma unroll 4
-    for (int j = gl; j < Lk; j += G) {
-      const float* kj = k + j * lm + hd * DH;
-      float sc = 0.f;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
-      m = fmaxf(m, sc);
-    }
-    for (int off = 1; off < G; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
     float l = 0.f;
+    constexpr int KR = DH <= 4 ? 12 : 1;  // keys per lane held in registers (small heads)
+    if (DH <= 4 && (Lk + G - 1) / G <= KR) {
+      // all of this lane's keys and values loaded up front (one LDS round trip instead of one per key);
+      // the same per-key arithmetic and order as the loop below, so the result is bitwise the same
+      float kr[KR][DH], vr[KR][DH];
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int j = min(gl + u * G, Lk - 1);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          kr[u][d] = k[j * lm + hd * DH + d];
+          vr[u][d] = v[j * lm + hd * DH + d];
+        }
+      }
+      float sc[KR];
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        sc[u] = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) sc[u] += qq[d] * kr[u][d];
+        if (gl + u * G < Lk) m = fmaxf(m, sc[u]);
+      }
+      for (int off = 1; off < G; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        if (gl + u * G >= Lk) break;
+        const float pj = __expf(sc[u] - m);
+        l += pj;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc[d] += pj * vr[u][d];
+      }
+    } else {
 #pragma unroll 4
-    for (int j = gl; j < Lk; j += G) {
-      const float* kj = k + j * lm + hd * DH;
-      float sc = 0.f;
+      for (int j = gl; j < Lk; j += G) {
+        const float* kj = k + j * lm + hd * DH;
+        float sc = 0.f;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
-      const float pj = __expf(sc - m);
-      l += pj;
-      const float* vj = v + j * lm + hd * DH;
+        for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
+        m = fmaxf(m, sc);
+      }
+      for (int off = 1; off < G; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+#pragma unroll 4
+      for (int j = gl; j < Lk; j += G) {
+        const float* kj = k + j * lm + hd * DH;
+        float sc = 0.f;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) acc[d] += pj * vj[d];
+        for (int d = 0; d < DH; ++d) sc += qq[d] * kj[d];
+        const float pj = __expf(sc - m);
+        l += pj;
+        const float* vj = v + j * lm + hd * DH;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc[d] += pj * vj[d];
+      }
     }
     for (int off = 1; off < G; off <<= 1) {
       l += __shfl_xor(l, off);
