@@ -238,6 +238,92 @@ __global__ __launch_bounds__(256) void coord_proj_kernel(ProjArgs pa, int TP, in
   }
 }
 
+// Register-tiled form (every M % 4 == 0): a thread owns 4 positions x 4 consecutive outputs and reads,
+// per k, one 16-byte weight quad (consecutive lanes = consecutive quads: conflict-free) and 4 source
+// values (broadcast over the 16 lanes sharing the positions; source rows padded by 4 floats so the 4
+// position groups of a wave land on distinct banks): 16 FMAs per 5 LDS reads instead of 1 per 2.  Each
+// output still accumulates bias + sum over k in k order with FMAs: bitwise equal to coord_proj_kernel.
+constexpr int PJ_TPT = 2;  // tasks (4 x 4 output tiles) per thread
+__global__ __launch_bounds__(256) void coord_proj4_kernel(ProjArgs pa, int TP, int KC) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const ProjJob& jb = pa.job[blockIdx.y];
+  const int n = blockIdx.z;
+  const int p0 = blockIdx.x * TP;
+  if (p0 >= jb.L) return;
+  const int np = min(TP, jb.L - p0), M = jb.M, K = jb.K, KCP = KC + 4;
+  float* ss = sm;              // [TP][KCP]
+  float* ws = sm + TP * KCP;   // [KC][M]
+  const int mq = M >> 2, ntask = ((np + 3) >> 2) * mq;
+  f4 acc[PJ_TPT][4];
+#pragma unroll
+  for (int u = 0; u < PJ_TPT; ++u) {
+    const int t = threadIdx.x + u * 256;
+    const int m4 = (t % mq) * 4;
+    const f4 b = (t < ntask && jb.b) ? *reinterpret_cast<const f4*>(jb.b + m4) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[u][q] = b;
+  }
+  const float* src = jb.src + (int64_t(n) * jb.L + p0) * K;
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    const int kc = min(KC, K - k0);
+    __syncthreads();
+    // 16-byte staging (K, kc, M multiples of 4), 8 quads per thread in flight per round: one round covers
+    // 32 KiB, so a chunk usually stages in one memory round trip
+    float* dummy = ws + KC * M;  // 4 floats past the weights
+    const int kq = kc >> 2, n1 = np * kq, n2 = kc * M / 4, nt = n1 + n2;
+    for (int e0 = 0; e0 < nt; e0 += 8 * 256) {
+      f4 v[8];
+      float* d[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + int(threadIdx.x) + 256 * u;
+        const bool s1 = e < n1;  // address selects only: every load unconditional
+        const int i = s1 ? e / kq : 0, c4 = s1 ? (e - i * kq) * 4 : 0;
+        const int e2 = s1 ? 0 : min(e - n1, n2 - 1);
+        const float* sp = s1 ? src + int64_t(i) * K + k0 + c4 : jb.wt + int64_t(k0) * M + 4 * e2;
+        d[u] = s1 ? ss + i * KCP + c4 : (e < nt ? ws + 4 * e2 : dummy);
+        v[u] = *reinterpret_cast<const f4*>(sp);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(d[u]) = v[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PJ_TPT; ++u) {
+      const int t = threadIdx.x + u * 256;
+      if (t >= ntask) break;
+      const int pi = (t / mq) * 4, m4 = (t % mq) * 4;
+      // rows past np read unstaged LDS: computed, never stored
+      const float* sr[4] = {ss + min(pi + 0, TP - 1) * KCP, ss + min(pi + 1, TP - 1) * KCP,
+                            ss + min(pi + 2, TP - 1) * KCP, ss + min(pi + 3, TP - 1) * KCP};
+      for (int c = 0; c < kc; ++c) {
+        const f4 w = *reinterpret_cast<const f4*>(ws + c * M + m4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float sv = sr[q][c];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[u][q][j] += sv * w[j];
+        }
+      }
+    }
+  }
+  float* dst = jb.dst + (int64_t(n) * jb.L + p0) * M;
+#pragma unroll
+  for (int u = 0; u < PJ_TPT; ++u) {
+    const int t = threadIdx.x + u * 256;
+    if (t >= ntask) break;
+    const int pi = (t / mq) * 4, m4 = (t % mq) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (pi + q >= np) break;
+      f4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = act_f(acc[u][q][j], jb.act);
+      *reinterpret_cast<f4*>(dst + (pi + q) * M + m4) = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- 3. attention + out proj
 struct AttJob {
   const float* q;   // [N][Lq][mid]
@@ -722,6 +808,23 @@ static int launch_proj(ProjJob* jobs, int nj, int N, hipStream_t s) {
     maxK = std::max(maxK, jobs[i].K);
   }
   FCE_CHECK(maxM <= 256 * 16, "coord projection: too many outputs");
+  bool m4 = true;
+  for (int i = 0; i < nj; ++i) m4 = m4 && jobs[i].M % 4 == 0 && jobs[i].K % 4 == 0;
+  const char* pe = getenv("FCE_COORD_PROJ1");  // diagnostics: the scalar projection kernel
+  if (m4 && maxM <= 1024 && !(pe && atoi(pe))) {
+    // 4 x 4 tiles, <= PJ_TPT per thread: TP positions with (TP / 4) (M / 4) <= 256 PJ_TPT
+    int TP = 4 * std::max(1, std::min(16, 256 * PJ_TPT / (maxM / 4)));
+    // fewer positions per block while the grid is short of ~1.5 blocks per CU (m 160^2, M 64: 288 -> 480
+    // blocks, 55 -> 47 us); below 32 the idle task slots cost more than the extra blocks gain
+    while (TP > 32 && int64_t((maxL + TP - 1) / TP) * nj * N < 384) TP /= 2;
+    const char* te = getenv("FCE_COORD_PJTP");  // diagnostics: positions per block
+    if (te && atoi(te) >= 4) TP = std::min(TP, atoi(te) & ~3);
+    const int KC = std::max(4, std::min({maxK, 128, (12288 - TP * 68) / maxM}) & ~3);  // <= 48 KiB
+    const size_t shm = (size_t(TP) * (KC + 4) + size_t(KC) * maxM + 4) * sizeof(float);
+    dim3 grid((maxL + TP - 1) / TP, nj, N);
+    FCE_LAUNCH(coord_proj4_kernel, grid, dim3(256), shm, s, pa, TP, KC);
+    return launch_status("coord_proj4_kernel");
+  }
   const int TP = std::max(1, std::min(16, 256 * 16 / maxM));                       // positions per block
   const int KC = std::max(1, std::min({maxK, 256, (8192 - TP * 64) / maxM}));      // <= 32 KiB of weights
   const size_t shm = (size_t(TP) * KC + size_t(KC) * maxM + 1) * sizeof(float);  // + the staging dummy
