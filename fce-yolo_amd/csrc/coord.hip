@@ -758,41 +758,59 @@ __global__ __launch_bounds__(CORE_THREADS) void coord_core_kernel(CoreArgs a) {
 // ---------------------------------------------------------------------------- 4. apply
 enum { GATE_BICOORD = 0, GATE_COORD = 1, GATE_ROW = 2 };
 
-// grid (row chunks, N*H): thread = (column, 8-channel group) of one row, 32-bit index math
-template <int MODE>
+// grid (row chunks of GPX * 256 elements, N*H): element = (column, 8-channel group) of one row, 32-bit
+// index math.  A thread takes GPX elements 256 apart and issues all their x and gate loads before any
+// math (GPX x more bytes in flight per wave: the kernel streams x once and y once at ~HBM rate).
+template <int MODE, int GPX>
 __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int xcs, _Float16* y, int ycs, int N,
                                                          int H, int W, int C, const float* g1, const float* g2) {
   const int CG = C / 8;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= W * CG) return;
-  {
-    const int xx = e / CG, g = e - xx * CG;
-    const int row = blockIdx.y, n = row / H, yy = row - n * H;
-    const int64_t pix = int64_t(row) * W + xx;
-    const h8 v = *reinterpret_cast<const h8*>(x + pix * xcs + g * 8);
-    const float* gh = g1 + (int64_t(n) * H + yy) * C + g * 8;
-    const f4 gh0 = *reinterpret_cast<const f4*>(gh), gh1 = *reinterpret_cast<const f4*>(gh + 4);
-    float gv[8] = {gh0[0], gh0[1], gh0[2], gh0[3], gh1[0], gh1[1], gh1[2], gh1[3]};
+  const int row = blockIdx.y, n = row / H, yy = row - n * H;
+  h8 v[GPX];
+  f4 ga[GPX][2], gb[GPX][2];
+  int xx[GPX], gg[GPX];
+  bool live[GPX];
+#pragma unroll
+  for (int k = 0; k < GPX; ++k) {
+    const int e = (blockIdx.x * GPX + k) * 256 + threadIdx.x;
+    live[k] = e < W * CG;
+    const int ec = live[k] ? e : 0;
+    xx[k] = ec / CG;
+    gg[k] = ec - xx[k] * CG;
+    const int64_t pix = int64_t(row) * W + xx[k];
+    v[k] = *reinterpret_cast<const h8*>(x + pix * xcs + gg[k] * 8);
+    const float* gh = g1 + (int64_t(n) * H + yy) * C + gg[k] * 8;
+    ga[k][0] = *reinterpret_cast<const f4*>(gh);
+    ga[k][1] = *reinterpret_cast<const f4*>(gh + 4);
+    if (MODE != GATE_ROW) {
+      const float* gw = g2 + (int64_t(n) * W + xx[k]) * C + gg[k] * 8;
+      gb[k][0] = *reinterpret_cast<const f4*>(gw);
+      gb[k][1] = *reinterpret_cast<const f4*>(gw + 4);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GPX; ++k) {
+    if (!live[k]) continue;
+    float gv[8] = {ga[k][0][0], ga[k][0][1], ga[k][0][2], ga[k][0][3], ga[k][1][0], ga[k][1][1], ga[k][1][2], ga[k][1][3]};
     float wv[8] = {1, 1, 1, 1, 1, 1, 1, 1};
     if (MODE != GATE_ROW) {
-      const float* gw = g2 + (int64_t(n) * W + xx) * C + g * 8;
-      const f4 gw0 = *reinterpret_cast<const f4*>(gw), gw1 = *reinterpret_cast<const f4*>(gw + 4);
-      wv[0] = gw0[0]; wv[1] = gw0[1]; wv[2] = gw0[2]; wv[3] = gw0[3];
-      wv[4] = gw1[0]; wv[5] = gw1[1]; wv[6] = gw1[2]; wv[7] = gw1[3];
+      wv[0] = gb[k][0][0]; wv[1] = gb[k][0][1]; wv[2] = gb[k][0][2]; wv[3] = gb[k][0][3];
+      wv[4] = gb[k][1][0]; wv[5] = gb[k][1][1]; wv[6] = gb[k][1][2]; wv[7] = gb[k][1][3];
     }
     h8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float r;
       if (MODE == GATE_BICOORD)
-        r = (float)v[j] * (1.0f / (1.0f + __expf(-(gv[j] + wv[j]))));
+        r = (float)v[k][j] * (1.0f / (1.0f + __expf(-(gv[j] + wv[j]))));
       else if (MODE == GATE_COORD)
-        r = (float)v[j] * gv[j] * wv[j];
+        r = (float)v[k][j] * gv[j] * wv[j];
       else
-        r = (float)v[j] * gv[j];
+        r = (float)v[k][j] * gv[j];
       o[j] = (_Float16)r;
     }
-    *reinterpret_cast<h8*>(y + pix * ycs + g * 8) = o;
+    const int64_t pix = int64_t(row) * W + xx[k];
+    *reinterpret_cast<h8*>(y + pix * ycs + gg[k] * 8) = o;
   }
 }
 
@@ -1058,15 +1076,18 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   }
   _Float16* yp = static_cast<_Float16*>(y.data) + y.coff;
   FCE_CHECK(int64_t(N) * H < 65536 * 1024, "coord attention: too many rows");
-  const dim3 grid((W * (d.oup / 8) + 255) / 256, N * H);
+  // 4 elements per thread on wide rows (m/l 160^2 x 512: 208 -> 183 us); 1 on narrow rows, where the
+  // 4-wide blocks leave too few of them (n 80^2 x 128: 22.5 vs 29 us)
+  const int gpx = W * (d.oup / 8) >= 4096 ? 4 : 1;
+  const dim3 grid((W * (d.oup / 8) + 256 * gpx - 1) / (256 * gpx), N * H);
   if (kind == 0)
-    FCE_LAUNCH(gate_apply_kernel<GATE_BICOORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
+    FCE_LAUNCH((gpx == 4 ? gate_apply_kernel<GATE_BICOORD, 4> : gate_apply_kernel<GATE_BICOORD, 1>), grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
                        d.oup, w.g1, w.g2);
   else if (kind == 1)
-    FCE_LAUNCH(gate_apply_kernel<GATE_COORD>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+    FCE_LAUNCH((gpx == 4 ? gate_apply_kernel<GATE_COORD, 4> : gate_apply_kernel<GATE_COORD, 1>), grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
                        w.g1, w.g2);
   else
-    FCE_LAUNCH(gate_apply_kernel<GATE_ROW>, grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
+    FCE_LAUNCH((gpx == 4 ? gate_apply_kernel<GATE_ROW, 4> : gate_apply_kernel<GATE_ROW, 1>), grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W, d.oup,
                        w.g1, w.g2);
   return launch_status("gate_apply_kernel");
 }
