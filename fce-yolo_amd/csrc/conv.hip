@@ -1273,7 +1273,8 @@ struct Tile3Geom {
   static constexpr int NQ = 4 * KP;
   static constexpr int NE = RI * CI * NQ, NL = (NE + 255) / 256;
   static constexpr int NA = AL ? CW * RC * 9 * KP * 64 : 0, NLA = (NA + 255) / 256;
-  static constexpr bool PF = AL ? NL + NLA <= 16 : NL <= 8;  // register prefetch of the next stage
+  // register prefetch of the next stage (rc 1 has the registers for 10 pieces: stride-2 rp 8 tiles)
+  static constexpr bool PF = AL ? NL + NLA <= 16 : NL <= (RC == 1 ? 10 : 8);
   static constexpr size_t lds = size_t(PF ? NL * 256 : NE) * 16 + size_t(AL ? (PF ? NLA * 256 : NA) : 0) * 16;
 };
 
@@ -2449,9 +2450,10 @@ static constexpr bool tile3al_ok(int s, int rc, int rp, int cw, int kp) {
          tile3_lds(s, rp, cw, kp) + size_t(cw) * rc * 9 * kp * 1024 <= 96 * 1024;
 }
 // rp = 8 (8 output rows per wave: every A fragment read from L2 feeds 8 MFMAs, the m/l-scale 3x3 convs
-// are L2-bound at rp <= 4) only with rc >= 2 and the couts split over 2 / 4 waves
+// are L2-bound at rp <= 4) with rc 1 (any cw: the weight stream per output pixel halves at 32 accumulator
+// registers) or with the couts split over 2 / 4 waves
 static bool tile3_ok(int s, int rc, int rp, int cw, int kp) {
-  return (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && rc >= 2 && cw >= 2)) &&
+  return (rc == 1 || rc == 2 || rc == 4) && (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && (rc == 1 || cw >= 2))) &&
          (cw == 1 || cw == 2 || cw == 4) && (kp == 1 || kp == 2) && rc * rp <= 32 &&
          tile3_lds(s, rp, cw, kp) <= 80 * 1024;
 }
@@ -2584,7 +2586,7 @@ static void launch_tile3_rc(const ConvArgs& a, int rp, int cw, int kp, bool al, 
     launch_tile3_w<S, RC, 2>(a, cw, kp, al, grid, s);
   else if (rp == 4)
     launch_tile3_w<S, RC, 4>(a, cw, kp, al, grid, s);
-  else if constexpr (RC >= 2) {  // rp == 8: cw 2 / 4 (tile3_ok), any cw with A in LDS (tile3al_ok)
+  else {  // rp == 8: rc 1 or cw 2 / 4 (tile3_ok), any cw with A in LDS (tile3al_ok)
     if (cw == 1)
       kp == 1 ? launch_tile3_k<S, RC, 8, 1, 1>(a, al, grid, s) : launch_tile3_k<S, RC, 8, 1, 2>(a, al, grid, s);
     else if (cw == 2)
