@@ -16,7 +16,7 @@
 //   D: lane l holds px = l&15, couts 4(l>>4)+0..3  -> 8-byte NHWC stores.
 #include <type_traits>
 
-#include "common.h"
+#include "conv_args.h"
 
 namespace fce {
 
@@ -112,41 +112,6 @@ int conv_pack(const fce_conv_desc& d, const float* w, void* out) {
 }
 
 // ============================================================================ dense MFMA kernel
-// 16 zero bytes: the source of every out-of-image / padded-K B fragment (static device memory is
-// zero-initialised)
-__device__ __attribute__((aligned(16))) _Float16 g_zero_line[8];
-
-struct ConvArgs {
-  const _Float16* x;  // input view base (already offset by coff)
-  int N, Hs, Ws, xcs;  // source buffer spatial size, channel stride
-  int Hin, Win;        // logical input size (Hs << up)
-  int up;
-  int cin, cout, stride;
-  int Ho, Wo, P;  // output spatial, pixels total
-  const _Float16* w;
-  const float* bias;
-  const _Float16* res;  // residual view base or null
-  int rcs;
-  void* y;  // output view base
-  int ycs;
-  int act;
-  const float* fw;
-  int fn, fi;
-  int cpt, nchunk, nsteps;  // K-steps of 32
-  int nalloc;               // fragments stored per cout tile (see dense_geom)
-  unsigned cmagic;          // ceil(2^32 / cpt) for c / cpt = umulhi(c, cmagic)
-  int gx, gy;               // logical grid: pixel tiles x cout tiles (launched 1-D, see kernel)
-  int vec_ok;
-  int stg;                  // LDS-tile 1x1 kernels: fp16 output staged through LDS, 16-byte stores
-  // fused Detect tail (OUT_DFL / OUT_CLS): pred (N, 4+nc, A) fp32
-  float* pred;
-  int det_A, det_a0, det_nc, det_hw, det_w;
-  float det_stride;
-  unsigned long long* det_best;  // per-anchor best-class key [N][A] (fce_detect_epi::best), or null
-};
-
-enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3, OUT_DFL = 4, OUT_CLS = 5 };
-
 // Software-pipeline depth: K-steps of fragments in flight per wave.  Small register tiles have little
 // MFMA work per step to cover a load's latency, so they keep more steps in flight (the summation
 // order over K is the same for every depth).
@@ -1182,75 +1147,6 @@ static int launch_pipe1(const ConvArgs& a0, int out_kind, int wp, hipStream_t s)
 // re-fetching the pixels from L2 as the implicit-GEMM kernel does.  A fragments: the same packed
 // layout (K-step = chunk * 9 + tap).  Per output element the K order (chunk-major, tap, channel)
 // is the implicit-GEMM kernel's, so both kernels give bitwise-identical results.
-// LDS image of a staged tile: pixel (r, c) at position u = r * CI + tile_col(c), its four 16-byte
-// channel pieces q at slot q ^ ((u >> 1) & 3).  For stride 2 the even input columns come first, then
-// the odd ones, so the 16 lanes of a B fragment (output columns col * 2 + kx) read 16 consecutive
-// positions for every tap; with the XOR every ds_read_b128 lane group then meets 16 distinct 16-byte
-// slots of the bank row (was 2-way at stride 1 and 4-way at stride 2).
-template <int S, int CI>
-__device__ __forceinline__ int tile_col(int c) {
-  if (S == 1) return c;
-  return (c & 1) ? (CI + 1) / 2 + (c >> 1) : (c >> 1);
-}
-
-// XCD-aware block order of the 3x3 tile kernels: the grid is 1-D (tiles x cout groups); block b runs on
-// XCD b % 8, so each XCD gets a contiguous range of logical blocks, cout groups innermost: the blocks that
-// stage the same input tile, and the neighbouring tiles that share its halo rows, hit one L2.
-__device__ __forceinline__ void tile_block(int gy, int& tile, int& cog) {
-  const int total = int(gridDim.x), b = int(blockIdx.x), per = total >> 3, body = per << 3;
-  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
-  tile = L / gy;
-  cog = L - tile * gy;
-}
-
-// Epilogue of the 3x3 tile kernels: acc[r][p] = cout tile cot0 + r x output row oy0 + p (16 columns
-// from ox0, lane col); bias, SiLU, optional residual, fp16 NHWC store.
-template <int RC, int RP>
-__device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP], int n, int oy0, int ox0, int cot0,
-                                            int col, int grp) {
-  const int cotiles = (a.cout + 15) >> 4;
-  const int ox = ox0 + col;
-  if (ox >= a.Wo) return;
-#pragma unroll
-  for (int r = 0; r < RC; ++r) {
-    const int co0 = (cot0 + r) * 16 + grp * 4;
-    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
-    float bz[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
-#pragma unroll
-    for (int p = 0; p < RP; ++p) {
-      const int oy = oy0 + p;
-      if (oy >= a.Ho) continue;
-      const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float tt = acc[r][p][j] + bz[j];
-        v[j] = a.act ? silu(tt) : tt;
-      }
-      _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
-      if (a.res) {
-        const _Float16* ro = a.res + pix * a.rcs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          const h4 rv = *reinterpret_cast<const h4*>(ro);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
-        } else {
-          for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
-        }
-      }
-      if (a.vec_ok && co0 + 3 < a.cout) {
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
-      } else {
-        for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
-      }
-    }
-  }
-}
-
 // Tile-kernel geometry (template): CW waves split the block's cout tiles (CW*RC of them), the other
 // 4/CW split its rows (RP rows each, TH = (4/CW)*RP); KP 32-channel chunks are staged per barrier
 // (KP = 2: 128 bytes per pixel, full-line loads, half the barriers).  Slot swizzle of the 4*KP pieces
@@ -2541,6 +2437,10 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
               out[n++] = 0x100 | rc | (rp << 4) | (cwl << 12) | ((kp - 1) << 14);
         }
     }
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box)  // big tile: 0x800 | wm << 4
+    for (int ab : {2, 3})
+      for (int wm : {1, 2})
+        if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 128 && tile3al_on())  // A in LDS: | 1 << 15
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
@@ -2926,6 +2826,12 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     rp = (tile >> 4) & 15;
     FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && out_kind == OUT_F16 && d.up == 0, "conv: bad 3x3 ring hint");
     return launch_ring3(a, rp, d.stride, s);
+  }
+  if (kind == 8) {  // big-tile LDS-DMA 3x3 kernel
+    const int wm = (tile >> 4) & 15, ab = ((tile >> 12) & 3) + 2;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xF) == 0 && big3_ok(d.stride, wm, ab),
+              "conv: bad big-tile 3x3 hint");
+    return launch_big3(a, wm, ab, d.stride, x.n, s);
   }
   if (kind == 1) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;

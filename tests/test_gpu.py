@@ -447,6 +447,8 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     # m/l 3x3s (A-in-LDS tile kernel, 0x81xx): partial cout groups, odd chunk counts, stride 2, residual
     (256, 256, 3, 1, 40, 40, True), (128, 80, 3, 2, 41, 37, False), (192, 128, 3, 1, 37, 29, True),
     (160, 48, 3, 1, 21, 19, False),
+    # big-tile LDS-DMA 3x3 (0x8x0): stride 2 with partial cout groups / edge tiles, residual
+    (128, 136, 3, 2, 41, 37, False), (96, 192, 3, 2, 33, 47, True), (64, 96, 3, 1, 19, 35, True),
 ]
 
 
