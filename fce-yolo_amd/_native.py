@@ -91,6 +91,21 @@ class C3k2Desc(C.Structure):
     ]
 
 
+class NmsOpts(C.Structure):
+    """fce_nms_opts: the non-default arguments of non_max_suppression (utils/nms.py:13-29)."""
+    _fields_ = [
+        ("conf_thres", C.c_float),
+        ("iou_thres", C.c_float),
+        ("max_det", C.c_int),
+        ("max_nms", C.c_int),
+        ("max_wh", C.c_float),
+        ("agnostic", C.c_int),
+        ("multi_label", C.c_int),
+        ("classes", C.c_void_p),
+        ("nclasses", C.c_int),
+    ]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _SZ = C.c_size_t
@@ -125,6 +140,8 @@ _SIGS = {
     "fce_nms_workspace_bytes": (_SZ, [_I, _I, _I]),
     "fce_nms": (_I, [_P, _I, _I, _I, C.c_float, C.c_float, _I, _I, C.c_float, _P, _SZ, _P, _P, _P, _P]),
     "fce_nms_best": (_I, [_P, _P, _I, _I, _I, C.c_float, C.c_float, _I, _I, C.c_float, _P, _SZ, _P, _P, _P, _P]),
+    "fce_nms_workspace_bytes_ex": (_SZ, [_I, _I, _I, C.POINTER(NmsOpts)]),
+    "fce_nms_ex": (_I, [_P, _P, _I, _I, _I, C.POINTER(NmsOpts), _P, _SZ, _P, _P, _P, _P]),
     "fce_copy": (_I, [_PT, _PT, _P]),
     "fce_net_create": (_P, []),
     "fce_net_destroy": (None, [_P]),

@@ -38,9 +38,10 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
 int detect_decode(const fce_tensor* box, const fce_tensor* cls, int nl, const float* strides, int reg_max,
                   float* out, hipStream_t s);
 size_t nms_ws_bytes(int n, int A, int max_nms);
+size_t nms_ws_bytes_ex(int n, int nc, int A, int max_nms, int multi);
 int nms(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou, int max_det,
-        int max_nms, float max_wh,
-        void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, hipStream_t s);
+        int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
+        hipStream_t s, int multi = 0, const int32_t* classes = nullptr, int nclasses = 0);
 
 bool c3k2_fused_ok(const fce_c3k2_desc& d);
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
@@ -168,6 +169,16 @@ int fce_nms_best(const float* pred, const unsigned long long* best, int n, int n
   FCE_CHECK(pred && best && dets && keep && counts, "fce_nms_best: null argument");
   FCE_GUARD(return nms(pred, best, n, nc, A, conf, iou, max_det, max_nms, max_wh, ws, wsb, dets, keep, counts,
                        S(stream));)
+}
+size_t fce_nms_workspace_bytes_ex(int n, int nc, int anchors, const fce_nms_opts* o) {
+  return o ? nms_ws_bytes_ex(n, nc, anchors, o->max_nms, o->multi_label) : 0;
+}
+int fce_nms_ex(const float* pred, const unsigned long long* best, int n, int nc, int A, const fce_nms_opts* o, void* ws,
+               size_t wsb, float* dets, int64_t* keep, int32_t* counts, void* stream) {
+  FCE_CHECK(pred && o && dets && keep && counts, "fce_nms_ex: null argument");
+  FCE_GUARD(return nms(pred, best, n, nc, A, o->conf_thres, o->iou_thres, o->max_det, o->max_nms,
+                       o->agnostic ? 0.f : o->max_wh, ws, wsb, dets, keep, counts, S(stream), o->multi_label,
+                       o->classes, o->nclasses);)
 }
 int fce_letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad_value, void* stream) {
   FCE_GUARD(return letterbox(imgs, n, dst, H, W, pad_value, S(stream));)

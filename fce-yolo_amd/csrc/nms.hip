@@ -47,16 +47,24 @@ static constexpr int POOL = 112 * 1024;
 static constexpr int OFF_KB = 32 * 1024, OFF_VA = 64 * 1024, OFF_VB = 80 * 1024, OFF_WC = 96 * 1024;
 static constexpr int OFF_KBOX = 32 * 1024, OFF_KAREA = 48 * 1024, OFF_KIDX = 52 * 1024;
 
+// Candidate capacity C: A (best class per anchor), or A * nc with multi_label (one candidate per
+// (anchor, class) above conf_thres).
 struct NmsWs {
   float* aconf;    // per-anchor best score    [A]   (nms_best_class_kernel)
   int* acls;       // per-anchor best class    [A]
-  int* cidx;       // candidate anchor index   [A]
-  float* cscore;   // candidate score          [A]
-  int* ccls;       // candidate class          [A]
-  float4* cbox;    // candidate class-offset xyxy [A]
-  float* carea;    // candidate area           [A]
-  uint64_t* keys;  // global sort keys         [P2]  (> RADIX_CAP candidates)
-  int* spos;       // sorted -> candidate pos  [M]   (> RADIX_CAP candidates)
+  int* cidx;       // candidate anchor index   [C]
+  float* cscore;   // candidate score          [C]
+  int* ccls;       // candidate class          [C]
+  float4* cbox;    // candidate class-offset xyxy [C]
+  float* carea;    // candidate area           [C]
+  uint64_t* keys;  // global sort keys         [P2 = next_pow2(C)]  (> RADIX_CAP candidates)
+  int* spos;       // sorted -> candidate pos  [M = min(C, max_nms)]   (> RADIX_CAP candidates)
+};
+
+// classes= filter (nms.py:128-132) as a bit mask over class ids < 1024; on == 0: every class
+struct NmsClassMask {
+  uint32_t w[32];
+  int on;
 };
 
 static int next_pow2(int v) {
@@ -65,14 +73,19 @@ static int next_pow2(int v) {
   return p;
 }
 
-static size_t nms_ws_per_image(int A, int max_nms) {
-  const size_t M = std::min(A, max_nms);
-  const size_t P2 = next_pow2(std::max(A, 1));
+static size_t nms_ws_per_image(int A, int C, int max_nms) {
+  const size_t M = std::min(C, max_nms);
+  const size_t P2 = next_pow2(std::max(C, 1));
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-  return al(size_t(A) * 4) * 6 + size_t(A) * 16 + P2 * 8 + al(M * 4);
+  return al(size_t(A) * 4) * 2 + al(size_t(C) * 4) * 4 + size_t(C) * 16 + P2 * 8 + al(M * 4);
 }
 
-size_t nms_ws_bytes(int n, int A, int max_nms) { return size_t(n) * nms_ws_per_image(A, max_nms); }
+static int nms_cap(int A, int nc, int multi) { return multi && nc > 1 ? A * nc : A; }
+
+size_t nms_ws_bytes(int n, int A, int max_nms) { return size_t(n) * nms_ws_per_image(A, A, max_nms); }
+size_t nms_ws_bytes_ex(int n, int nc, int A, int max_nms, int multi) {
+  return size_t(n) * nms_ws_per_image(A, nms_cap(A, nc, multi), max_nms);
+}
 
 __device__ __forceinline__ int next_pow2_dev(int v) {
   int p = 1;
@@ -80,20 +93,21 @@ __device__ __forceinline__ int next_pow2_dev(int v) {
   return p;
 }
 
-__device__ NmsWs carve(char* p, int A, int max_nms) {
+__device__ NmsWs carve(char* p, int A, int C) {
   NmsWs w;
-  const int P2 = next_pow2_dev(max(A, 1));
+  const int P2 = next_pow2_dev(max(C, 1));
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const size_t a4 = al(size_t(A) * 4);
+  const size_t a4 = al(size_t(A) * 4), c4 = al(size_t(C) * 4);
   w.aconf = reinterpret_cast<float*>(p);
   w.acls = reinterpret_cast<int*>(p + a4);
-  w.cidx = reinterpret_cast<int*>(p + 2 * a4);
-  w.cscore = reinterpret_cast<float*>(p + 3 * a4);
-  w.ccls = reinterpret_cast<int*>(p + 4 * a4);
-  w.carea = reinterpret_cast<float*>(p + 5 * a4);
-  p += 6 * a4;
+  p += 2 * a4;
+  w.cidx = reinterpret_cast<int*>(p);
+  w.cscore = reinterpret_cast<float*>(p + c4);
+  w.ccls = reinterpret_cast<int*>(p + 2 * c4);
+  w.carea = reinterpret_cast<float*>(p + 3 * c4);
+  p += 4 * c4;
   w.cbox = reinterpret_cast<float4*>(p);
-  p += size_t(A) * 16;
+  p += size_t(C) * 16;
   w.keys = reinterpret_cast<uint64_t*>(p);
   p += size_t(P2) * 8;
   w.spos = reinterpret_cast<int*>(p);
@@ -118,6 +132,30 @@ __device__ int block_scan(int flag, int* wsum, int* total) {
   }
   __syncthreads();
   return wsum[wv] + before;
+}
+
+// block-wide exclusive scan of non-negative counts
+__device__ int block_scan_int(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < NWAVES; ++i) {
+      const int t = wsum[i];
+      wsum[i] = acc;
+      acc += t;
+    }
+    *total = acc;
+  }
+  __syncthreads();
+  return wsum[wv] + x - v;
 }
 
 __device__ void bitonic_desc(uint64_t* k, int n2) {
@@ -271,7 +309,7 @@ __global__ __launch_bounds__(256) void nms_best_class_kernel(const float* pred, 
       bj = c;
     }
   }
-  NmsWs w = carve(ws + size_t(n) * ws_per_image, A, max_nms);
+  NmsWs w = carve(ws + size_t(n) * ws_per_image, A, A);
   w.aconf[a] = best;
   w.acls[a] = bj;
 }
@@ -280,7 +318,8 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
                                                           int A, float conf_thres,
                                                           float iou_thres, int max_det, int max_nms, float max_wh,
                                                           char* ws, size_t ws_per_image, float* dets, int64_t* keep,
-                                                          int32_t* counts, int stop) {
+                                                          int32_t* counts, int stop, int multi, int cap,
+                                                          NmsClassMask cm) {
   __shared__ __attribute__((aligned(16))) char pool[POOL];
   __shared__ int wsum[NWAVES];
   __shared__ int tile_idx[TILE];
@@ -292,11 +331,41 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
   const int n = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* P = pred + int64_t(n) * (4 + nc) * A;
-  NmsWs w = carve(ws + size_t(n) * ws_per_image, A, max_nms);
+  NmsWs w = carve(ws + size_t(n) * ws_per_image, A, cap);
+  auto allowed = [&](int j) { return !cm.on || (j < 1024 && ((cm.w[j >> 5] >> (j & 31)) & 1u)); };
 
   // ---- 1. candidates in anchor order (+ their class-offset boxes)
   int base = 0, degenerate = 0;
-  for (int a0 = 0; a0 < A; a0 += NMS_THREADS) {
+  auto put = [&](int c, int a, float score, int j, float cx, float cy, float hw, float hh) {
+    w.cidx[c] = a;
+    w.cscore[c] = score;
+    w.ccls[c] = j;
+    const float off = (float)j * max_wh;
+    const float bx1 = (cx - hw) + off, by1 = (cy - hh) + off, bx2 = (cx + hw) + off, by2 = (cy + hh) + off;
+    w.cbox[c] = make_float4(bx1, by1, bx2, by2);
+    const float ar = (bx2 - bx1) * (by2 - by1);
+    w.carea[c] = ar;
+    degenerate |= !(ar > 0.0f) || !isfinite(ar);
+  };
+  // multi_label (nms.py:116-120): torch.where(cls > conf_thres) in (anchor, class) order, then classes=
+  for (int a0 = 0; multi && a0 < A; a0 += NMS_THREADS) {
+    const int a = a0 + threadIdx.x;
+    int cnt = 0;
+    if (a < A)
+      for (int j = 0; j < nc; ++j) cnt += (P[int64_t(4 + j) * A + a] > conf_thres) && allowed(j);
+    int c = base + block_scan_int(cnt, wsum, &s_total);
+    if (cnt) {
+      const float cx = P[a], cy = P[int64_t(1) * A + a];
+      const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
+      for (int j = 0; j < nc; ++j) {
+        const float v = P[int64_t(4 + j) * A + a];
+        if (v > conf_thres && allowed(j)) put(c++, a, v, j, cx, cy, hw, hh);
+      }
+    }
+    base += s_total;
+    __syncthreads();
+  }
+  for (int a0 = 0; !multi && a0 < A; a0 += NMS_THREADS) {
     const int a = a0 + threadIdx.x;
     float best = -INFINITY;
     int bj = 0;
@@ -310,21 +379,12 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
         bj = w.acls[a];
       }
     }
-    const int flag = (a < A) && (best > conf_thres);
+    const int flag = (a < A) && (best > conf_thres) && allowed(bj);
     const int pos = block_scan(flag, wsum, &s_total);
     if (flag) {
-      const int c = base + pos;
-      w.cidx[c] = a;
-      w.cscore[c] = best;
-      w.ccls[c] = bj;
       const float cx = P[a], cy = P[int64_t(1) * A + a];
       const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
-      const float off = (float)bj * max_wh;
-      const float bx1 = (cx - hw) + off, by1 = (cy - hh) + off, bx2 = (cx + hw) + off, by2 = (cy + hh) + off;
-      w.cbox[c] = make_float4(bx1, by1, bx2, by2);
-      const float ar = (bx2 - bx1) * (by2 - by1);
-      w.carea[c] = ar;
-      degenerate |= !(ar > 0.0f) || !isfinite(ar);
+      put(base + pos, a, best, bj, cx, cy, hw, hh);
     }
     base += s_total;
     __syncthreads();
@@ -623,20 +683,32 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
 
 int nms(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou, int max_det,
         int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
-        hipStream_t s) {
+        hipStream_t s, int multi, const int32_t* classes, int nclasses) {
   FCE_CHECK(nc >= 1 && nc <= 65535 && A >= 0 && max_det >= 1 && max_nms >= 1, "nms: bad sizes");
   FCE_CHECK(max_nms <= REMOVED_CAP, "nms: max_nms > 32768 unsupported");
   FCE_CHECK(conf >= 0.f && conf <= 1.f && iou >= 0.f && iou <= 1.f, "nms: thresholds must be in [0, 1]");
+  FCE_CHECK(nclasses >= 0 && (nclasses == 0 || classes), "nms: classes list");
+  multi = multi && nc > 1;  // nms.py:96 multi_label &= nc > 1
+  FCE_CHECK(!multi || int64_t(A) * nc < (int64_t(1) << 30), "nms: multi_label candidate capacity too large");
+  NmsClassMask cm{};
+  cm.on = classes != nullptr;
+  if (classes) {
+    FCE_CHECK(nc <= 1024, "nms: classes filter supports nc <= 1024");
+    for (int i = 0; i < nclasses; ++i)
+      if (classes[i] >= 0 && classes[i] < nc) cm.w[classes[i] >> 5] |= 1u << (classes[i] & 31);
+  }
   if (n == 0) return FCE_OK;
-  const size_t per = nms_ws_per_image(A, max_nms);
+  const int cap = nms_cap(A, nc, multi);
+  const size_t per = nms_ws_per_image(A, cap, max_nms);
   FCE_CHECK(ws && ws_bytes >= per * n, "nms: workspace too small");
   const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
   const int stop = stop_env ? atoi(stop_env) : 0;
-  if (A > 0 && !best)  // else the keys came from the Detect cls epilogue (fce_nms_best)
+  if (multi) best = nullptr;  // candidates come from every class row
+  if (A > 0 && !best && !multi)  // else the keys came from the Detect cls epilogue (fce_nms_best)
     FCE_LAUNCH(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);
   FCE_LAUNCH(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, best, nc, A, conf, iou, max_det, max_nms, max_wh,
-                     static_cast<char*>(ws), per, dets, keep, counts, stop);
+                     static_cast<char*>(ws), per, dets, keep, counts, stop, multi, cap, cm);
   return launch_status("nms_kernel");
 }
 

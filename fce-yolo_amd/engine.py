@@ -140,10 +140,22 @@ class Engine:
 class NMS:
     """Device NMS with persistent workspace/outputs (graph-capturable)."""
 
-    def __init__(self, batch, anchors, nc, device, conf=0.25, iou=0.7, max_det=300, max_nms=30000, max_wh=7680):
+    def __init__(self, batch, anchors, nc, device, conf=0.25, iou=0.7, max_det=300, max_nms=30000, max_wh=7680,
+                 classes=None, agnostic=False, multi_label=False):
+        """`classes` / `agnostic` / `multi_label`: the non-default arguments of nms.py:13-29 (fce_nms_ex)."""
         self.batch, self.anchors, self.nc = batch, anchors, nc
         self.conf, self.iou, self.max_det, self.max_nms, self.max_wh = conf, iou, max_det, max_nms, max_wh
-        nb = N.lib().fce_nms_workspace_bytes(batch, anchors, max_nms)
+        self.opts = None
+        if classes is not None or agnostic or multi_label:
+            cls = [int(c) for c in (classes.tolist() if hasattr(classes, "tolist") else classes)] \
+                if classes is not None else None
+            self._classes = (C.c_int32 * max(len(cls), 1))(*cls) if cls is not None else None
+            self.opts = N.NmsOpts(conf, iou, max_det, max_nms, float(max_wh), int(bool(agnostic)),
+                                  int(bool(multi_label)), C.cast(self._classes, C.c_void_p) if cls is not None else None,
+                                  len(cls) if cls is not None else 0)
+            nb = N.lib().fce_nms_workspace_bytes_ex(batch, nc, anchors, C.byref(self.opts))
+        else:
+            nb = N.lib().fce_nms_workspace_bytes(batch, anchors, max_nms)
         self.ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
         # outputs packed in one buffer (keep | dets | counts), so a multi-GPU gather is one collective
         self.buf = torch.zeros(self.packed_bytes(batch, max_det), dtype=torch.uint8, device=device)
@@ -169,6 +181,13 @@ class NMS:
         assert pred.is_contiguous() and pred.dtype == torch.float32 and tuple(pred.shape) == (
             self.batch, 4 + self.nc, self.anchors)
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        if self.opts is not None:
+            if best is not None:
+                assert best.dtype == torch.int64 and tuple(best.shape) == (self.batch, self.anchors)
+            N.call("fce_nms_ex", pred.data_ptr(), best.data_ptr() if best is not None else None, self.batch, self.nc,
+                   self.anchors, C.byref(self.opts), self.ws.data_ptr(), self.ws.numel(), self.dets.data_ptr(),
+                   self.keep.data_ptr(), self.counts.data_ptr(), stream)
+            return self.dets, self.keep, self.counts
         args = (self.batch, self.nc, self.anchors, self.conf, self.iou, self.max_det, self.max_nms,
                 float(self.max_wh), self.ws.data_ptr(), self.ws.numel(), self.dets.data_ptr(), self.keep.data_ptr(),
                 self.counts.data_ptr(), stream)
@@ -185,13 +204,15 @@ class NMS:
 
 
 def non_max_suppression(pred: torch.Tensor, conf_thres=0.25, iou_thres=0.7, max_det=300, max_nms=30000, max_wh=7680,
-                        return_idxs=False):
-    """nms.py:13-166 on the device: list of (k, 6) [x1,y1,x2,y2,conf,cls] per image (+ kept anchor indices)."""
+                        return_idxs=False, classes=None, agnostic=False, multi_label=False):
+    """nms.py:13-166 on the device: list of (k, 6) [x1,y1,x2,y2,conf,cls] per image (+ kept anchor indices).
+    `classes`, `agnostic`, `multi_label` as in the reference (fce_nms_ex)."""
     if pred.device.type != "cuda":
         raise RuntimeError("non_max_suppression: ROCm device tensor required (no CPU fallback)")
     pred = pred.float().contiguous()
     b, no, a = pred.shape
-    nms = NMS(b, a, no - 4, pred.device, conf_thres, iou_thres, max_det, max_nms, max_wh)
+    nms = NMS(b, a, no - 4, pred.device, conf_thres, iou_thres, max_det, max_nms, max_wh, classes=classes,
+              agnostic=agnostic, multi_label=multi_label)
     nms(pred)
     dets, keep = nms.results()
     return (dets, keep) if return_idxs else dets

@@ -70,12 +70,12 @@ def device_postprocess(predictor):
             end2end=False, return_idxs=False):
         """The signature of utils/nms.py:13-29; argument combinations off the device path go to `orig`."""
         pred = prediction[0] if isinstance(prediction, (list, tuple)) else prediction
-        if (classes is not None or agnostic or multi_label or len(labels) or nc or rotated or end2end
-                or pred.device.type != "cuda"):
+        if len(labels) or nc or rotated or end2end or pred.device.type != "cuda":
             return orig(prediction, conf_thres=conf_thres, iou_thres=iou_thres, classes=classes, agnostic=agnostic,
                         multi_label=multi_label, labels=labels, max_det=max_det, nc=nc, max_time_img=max_time_img,
                         max_nms=max_nms, max_wh=max_wh, rotated=rotated, end2end=end2end, return_idxs=return_idxs)
-        return non_max_suppression(pred, conf_thres, iou_thres, max_det, max_nms, max_wh, return_idxs)
+        return non_max_suppression(pred, conf_thres, iou_thres, max_det, max_nms, max_wh, return_idxs,
+                                   classes=classes, agnostic=agnostic, multi_label=multi_label)
 
     nms_mod.non_max_suppression = nms
     return orig

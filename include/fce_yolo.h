@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 3
+#define FCE_ABI_VERSION 4
 
 /* status codes */
 #define FCE_OK 0
@@ -214,6 +214,25 @@ int fce_nms(const float* pred, int n, int nc, int anchors, float conf_thres, flo
 int fce_nms_best(const float* pred, const unsigned long long* best, int n, int nc, int anchors, float conf_thres,
                  float iou_thres, int max_det, int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets,
                  int64_t* keep, int32_t* counts, void* stream);
+
+/* Non-default arguments of non_max_suppression (utils/nms.py:13-29), ABI v4:
+ *   agnostic     nms.py:141   class offset c = cls * 0 (one NMS over all classes);
+ *   multi_label  nms.py:116-120  one candidate per (anchor, class) with score > conf_thres, in (anchor, class)
+ *                order (torch.where), when nc > 1; the workspace then holds anchors * nc candidates;
+ *   classes      nms.py:128-132  keep only candidates whose class is in the host list (class ids < 1024).
+ * best (optional, the forward's best-class keys) is ignored with multi_label.  Bit-exact with the reference
+ * for distinct scores, like fce_nms. */
+typedef struct fce_nms_opts {
+  float conf_thres, iou_thres;
+  int max_det, max_nms;
+  float max_wh;
+  int agnostic, multi_label;
+  const int32_t* classes; /* host array, or NULL for every class */
+  int nclasses;
+} fce_nms_opts;
+size_t fce_nms_workspace_bytes_ex(int n, int nc, int anchors, const fce_nms_opts* o);
+int fce_nms_ex(const float* pred, const unsigned long long* best, int n, int nc, int anchors, const fce_nms_opts* o,
+               void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts, void* stream);
 
 /* ---------------------------------------------------------------- layout / dtype edges */
 /* dst = src with layout / dtype conversion (same n,c,h,w). */

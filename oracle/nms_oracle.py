@@ -1,7 +1,7 @@
 """numpy restatement of the reference NMS.  TEST INFRASTRUCTURE ONLY.
 
-Follows ``ultralytics/utils/nms.py:13-166`` (``non_max_suppression`` with the predict
-defaults: multi_label=False, agnostic=False, classes=None, no a-priori labels),
+Follows ``ultralytics/utils/nms.py:13-166`` (``non_max_suppression``, including the
+``classes`` / ``agnostic`` / ``multi_label`` arguments; no a-priori labels),
 ``ultralytics/utils/ops.py:224-240`` (``xywh2xyxy``) and ``nms.py:239-296``
 (``TorchNMS.nms``, the backend taken when torchvision is not imported, Q10).
 All arithmetic is float32 in the reference's operation order so kept indices are
@@ -56,11 +56,17 @@ def greedy_nms(boxes: np.ndarray, scores: np.ndarray, iou_thres: float) -> np.nd
     return np.asarray(keep, np.int64)
 
 
-def non_max_suppression(pred: np.ndarray, conf_thres=0.25, iou_thres=0.7, max_det=300, max_nms=30000, max_wh=7680):
-    """nms.py:13-166 for a (B, 4+nc, A) prediction.  Returns (dets list of (k,6), keep-index list)."""
+def non_max_suppression(pred: np.ndarray, conf_thres=0.25, iou_thres=0.7, max_det=300, max_nms=30000, max_wh=7680,
+                        classes=None, agnostic=False, multi_label=False):
+    """nms.py:13-166 for a (B, 4+nc, A) prediction.  Returns (dets list of (k,6), keep-index list).
+
+    classes / agnostic / multi_label follow nms.py:116-141: multi_label (when nc > 1) makes one candidate per
+    (anchor, class) with score > conf_thres in torch.where's (anchor, class) order; classes keeps candidates
+    whose class is listed; agnostic drops the per-class box offset."""
     pred = np.asarray(pred, np.float32)
     bs, no, A = pred.shape
     nc = no - 4
+    multi_label = bool(multi_label) and nc > 1  # nms.py:96
     dets, keeps = [], []
     for b in range(bs):
         x = pred[b].T  # (A, 84)
@@ -73,14 +79,21 @@ def non_max_suppression(pred: np.ndarray, conf_thres=0.25, iou_thres=0.7, max_de
             keeps.append(np.zeros((0,), np.int64))
             continue
         box = xywh2xyxy(x[:, :4])
-        j = x[:, 4:].argmax(1)
-        conf = x[np.arange(x.shape[0]), 4 + j]
-        filt = conf > np.float32(conf_thres)
-        box, conf, j, idx = box[filt], conf[filt], j[filt], idx[filt]
+        if multi_label:
+            i, j = np.nonzero(x[:, 4:] > np.float32(conf_thres))  # row-major, like torch.where
+            box, conf, idx = box[i], x[i, 4 + j], idx[i]
+        else:
+            j = x[:, 4:].argmax(1)
+            conf = x[np.arange(x.shape[0]), 4 + j]
+            filt = conf > np.float32(conf_thres)
+            box, conf, j, idx = box[filt], conf[filt], j[filt], idx[filt]
+        if classes is not None:
+            filt = np.isin(j, np.asarray(classes, np.int64))
+            box, conf, j, idx = box[filt], conf[filt], j[filt], idx[filt]
         if box.shape[0] > max_nms:
             o = np.argsort(-conf, kind="stable")[:max_nms]
             box, conf, j, idx = box[o], conf[o], j[o], idx[o]
-        c = j.astype(np.float32) * np.float32(max_wh)
+        c = j.astype(np.float32) * np.float32(0 if agnostic else max_wh)
         k = greedy_nms(box + c[:, None], conf, iou_thres)[:max_det]
         dets.append(np.concatenate([box[k], conf[k, None], j[k, None].astype(np.float32)], 1))
         keeps.append(idx[k])

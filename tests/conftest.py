@@ -58,6 +58,24 @@ def nms_fx():
 
 
 @pytest.fixture(scope="session")
+def nms_opts_fx():
+    return _Npz(GOLDEN / "nms_opts.npz")
+
+
+NMS_OPT_CASES = ["agnostic", "classes", "classes_absent", "multi", "multi_classes", "multi_agnostic", "multi_small",
+                 "multi_big"]
+
+
+def nms_opt_case(fx_all, name):
+    """(pred, options dict, [(det, keep) per image]) of one nms_opts.npz case (make_golden_nms_opts.py)."""
+    fx = fx_all.group(name)
+    opts = json.loads(bytes(fx["opts"]).decode())
+    pred = fx_all.group("pred")[opts.pop("pred")]
+    exp = [(fx[f"det{b}"].reshape(-1, 6), fx[f"keep{b}"].reshape(-1).astype(np.int64)) for b in range(pred.shape[0])]
+    return pred, opts, exp
+
+
+@pytest.fixture(scope="session")
 def device():
     if not torch.cuda.is_available():
         pytest.fail("GPU test run without a visible ROCm device")

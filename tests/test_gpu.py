@@ -16,6 +16,7 @@ import pytest
 import torch
 
 import cases
+from conftest import NMS_OPT_CASES, nms_opt_case
 from fce_yolo_amd import _native as N
 from fce_yolo_amd import modules as M
 from fce_yolo_amd.engine import NMS, Engine, Pipeline, non_max_suppression
@@ -281,6 +282,26 @@ def test_nms_bit_exact_vs_reference(name, nms_fx, device):
     for b in range(pred.shape[0]):
         assert np.array_equal(keep[b].cpu().numpy(), fx[f"keep{b}"].reshape(-1).astype(np.int64)), b
         assert np.array_equal(dets[b].cpu().numpy(), fx[f"det{b}"].reshape(-1, 6)), b
+
+
+@pytest.mark.parametrize("name", NMS_OPT_CASES)
+def test_nms_options_bit_exact_vs_reference(name, nms_opts_fx, device):
+    """fce_nms_ex (classes / agnostic / multi_label, nms.py:116-141): kept anchors and rows bit-exact against the
+    reference's outputs; with best-class keys built like the Detect epilogue's too (ignored by multi_label)."""
+    pred, opts, exp = nms_opt_case(nms_opts_fx, name)
+    pt = torch.from_numpy(pred).to(device)
+    dets, keep = non_max_suppression(pt, 0.25, 0.7, 300, return_idxs=True, **opts)
+    for b, (d, k) in enumerate(exp):
+        assert np.array_equal(keep[b].cpu().numpy(), k), b
+        assert np.array_equal(dets[b].cpu().numpy(), d), b
+    sc, cl = pt[:, 4:].max(1)  # first maximum, like the cls epilogue's keys
+    best = ((sc.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF) << 32) | (0xFFFFFFFF - cl)
+    b_, a_ = pred.shape[0], pred.shape[2]
+    nms = NMS(b_, a_, pred.shape[1] - 4, device, 0.25, 0.7, 300, **opts)
+    nms(pt, best.contiguous())
+    d2, k2 = nms.results()
+    for b, (d, k) in enumerate(exp):
+        assert np.array_equal(k2[b].cpu().numpy(), k) and np.array_equal(d2[b].cpu().numpy(), d), b
 
 
 def test_nms_on_reference_model_output(e2e_fx, device):

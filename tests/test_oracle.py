@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import cases
+from conftest import NMS_OPT_CASES, nms_opt_case
 from oracle import nms_oracle
 from oracle.parse import parse
 
@@ -72,6 +73,16 @@ def test_oracle_nms_bit_exact(name, nms_fx):
     for b in range(fx["pred"].shape[0]):
         assert np.array_equal(keeps[b], fx[f"keep{b}"].reshape(-1).astype(np.int64)), b
         assert np.array_equal(dets[b], fx[f"det{b}"].reshape(-1, 6)), b
+
+
+@pytest.mark.parametrize("name", NMS_OPT_CASES)
+def test_oracle_nms_options_bit_exact(name, nms_opts_fx):
+    """classes / agnostic / multi_label (nms.py:116-141) against the reference's outputs."""
+    pred, opts, exp = nms_opt_case(nms_opts_fx, name)
+    dets, keeps = nms_oracle.non_max_suppression(pred, **opts)
+    for b, (d, k) in enumerate(exp):
+        assert np.array_equal(keeps[b], k), b
+        assert np.array_equal(dets[b], d), b
 
 
 def test_oracle_nms_on_model_output(e2e_fx):
