@@ -2828,10 +2828,11 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     return launch_ring3(a, rp, d.stride, s);
   }
   if (kind == 8) {  // big-tile LDS-DMA 3x3 kernel
-    const int wm = (tile >> 4) & 15, ab = ((tile >> 12) & 3) + 2;
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xF) == 0 && big3_ok(d.stride, wm, ab),
+    const int wm = (tile >> 4) & 15, ab = ((tile >> 12) & 1) + 2, nw = 4;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xF) == 0 && (tile >> 13) == 0 &&
+                  big3_ok(d.stride, wm, ab, nw),
               "conv: bad big-tile 3x3 hint");
-    return launch_big3(a, wm, ab, d.stride, x.n, s);
+    return launch_big3(a, wm, ab, nw, d.stride, x.n, s);
   }
   if (kind == 1) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;

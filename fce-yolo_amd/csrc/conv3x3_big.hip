@@ -1,6 +1,8 @@
 // Big-tile 3x3 convolution fed by LDS-DMA (gfx950 global_load_lds_dwordx4); the m/l-scale 3x3 convs.
 // Replaces (reference, ultralytics/): nn/modules/conv.py:39-89 Conv.forward_fuse (3x3, BN folded by
 // utils/torch_utils.py:237-267) for cin % 32 == 0.  Variant code 0x800 | wm << 4 of fce_conv2d_variant.
+#include <vector>
+
 #include "conv_args.h"
 
 namespace fce {
@@ -16,9 +18,9 @@ namespace fce {
 // channel piece q ^ ((u >> 1) & 3); the read side applies the same involution).  Out-of-image pixels and the
 // padding of the last instruction read the zero line.  K order (chunk, tap) and the fragment layouts are the
 // implicit-GEMM kernel's: bitwise identical to every other variant.
-template <int S, int WM, int AB>
+template <int S, int WM, int AB, int NW = 4>
 struct Big3Geom {
-  static constexpr int WN = 4 / WM, TW = 16, TH = WN * 4;
+  static constexpr int WN = NW / WM, TW = 16, TH = WN * 4;
   static constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
   static constexpr int NPX = RI * CI;                   // staged input pixels per chunk (64 B each)
   static constexpr int BINS = (NPX * 4 + 63) / 64;      // 1 KiB DMA instructions for the input tile
@@ -52,9 +54,11 @@ __device__ __forceinline__ void vm_wait(int n) {
 // (c, 1).  Each wave waits with a counted vmcnt for exactly the copies the coming stage reads (its own
 // copies are retired in issue order; the raw barrier then publishes every wave's), so the copies issued
 // later stay in flight across the barrier.
-template <int S, int WM, int AB>
-__global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
-  using G = Big3Geom<S, WM, AB>;
+// TM (diagnostics, FCE_BIG3_TIMING=1): per wave, the clocks spent waiting for a stage (vmcnt + barrier) and
+// computing it, summed over the stages, for the first 4096 blocks.
+template <int S, int WM, int AB, int NW, bool TM>
+__global__ __launch_bounds__(NW * 64, 2) void conv3x3_big_kernel(ConvArgs a, unsigned long long* tm) {
+  using G = Big3Geom<S, WM, AB, NW>;
   constexpr int WN = G::WN, TW = G::TW, TH = G::TH, CI = G::CI, NPX = G::NPX;
   constexpr int BINS = G::BINS, AINS = G::AINS, AH8 = G::AH8, BH8 = G::BH8;
   extern __shared__ __attribute__((aligned(16))) h8 big3_smem[];  // [A0 | A1 (| A2) | B0 | B1], one array
@@ -79,12 +83,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
   h8* const bbase = big3_smem + AB * AH8;
 
   // input-tile pieces this lane copies (fixed over chunks): pixel offset in the image, or -1 (zero line)
-  constexpr int BPW = (BINS + 3) / 4;  // DMA instructions per wave for the input tile (some waves one fewer)
-  const int nb = wave + 4 * (BPW - 1) < BINS ? BPW : BPW - 1;
+  constexpr int BPW = (BINS + NW - 1) / NW;  // DMA instructions per wave for the input tile (some waves one fewer)
+  const int nb = wave + NW * (BPW - 1) < BINS ? BPW : BPW - 1;
   int64_t boff[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
-    const int e = (wave + 4 * j) * 64 + lane;
+    const int e = (wave + NW * j) * 64 + lane;
     const int u = e >> 2, slot = e & 3;
     boff[j] = -1;
     if (u < NPX) {
@@ -95,12 +99,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
       if (iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws) boff[j] = (int64_t(iy) * a.Ws + ix) * a.xcs + q * 8;
     }
   }
-  // weight rows this lane copies: instruction i = wave + 4 j -> cout tile i / 3, tap i % 3
-  constexpr int APW = AINS / 4;
+  // weight rows this lane copies: instruction i = wave + NW j -> cout tile i / 3, tap i % 3
+  constexpr int APW = (AINS + NW - 1) / NW;
+  const int na = wave + NW * (APW - 1) < AINS ? APW : APW - 1;
   const h8* asrc[APW];
 #pragma unroll
   for (int j = 0; j < APW; ++j) {
-    const int i = wave + 4 * j, r = i / 3, kx = i - r * 3;
+    const int i = min(wave + NW * j, AINS - 1), r = i / 3, kx = i - r * 3;
     const int ct = min(ct_blk + r, cotiles - 1);
     asrc[j] = wts + (size_t(ct) * a.nalloc + kx) * 64 + lane;
   }
@@ -108,16 +113,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
     const int c = s / 3, ky = s - c * 3;
     h8* ab = big3_smem + (s % AB) * AH8;
 #pragma unroll
-    for (int j = 0; j < APW; ++j) glds16(asrc[j] + (c * 9 + ky * 3) * 64, ab + (wave + 4 * j) * 64);
+    for (int j = 0; j < APW; ++j)
+      if (wave + NW * j < AINS) glds16(asrc[j] + (c * 9 + ky * 3) * 64, ab + (wave + NW * j) * 64);
   };
   auto issue_b = [&](int c) {
     h8* bb = bbase + (c & 1) * BH8;
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
-      if (wave + 4 * j < BINS) {
+      if (wave + NW * j < BINS) {
         const void* src = boff[j] >= 0 ? static_cast<const void*>(xn + boff[j] + c * 32)
                                        : static_cast<const void*>(g_zero_line);
-        glds16(src, bb + (wave + 4 * j) * 64);
+        glds16(src, bb + (wave + NW * j) * 64);
       }
     }
   };
@@ -130,19 +136,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
   issue_a(0);
   issue_b(0);
   if (AB == 3 && nst > 1) issue_a(1);
+  unsigned long long t_start = 0, t_wait = 0, t_comp = 0, t0 = 0;
+  if constexpr (TM) t_start = __builtin_amdgcn_s_memtime();
   for (int s = 0; s < nst; ++s) {
+    if constexpr (TM) t0 = __builtin_amdgcn_s_memtime();
     const int c = s / 3, ky = s - c * 3;
     // copies this wave may leave in flight: those issued after the last one stage s reads
     int allow;
     if (AB == 2) {
       allow = (ky == 1 && c + 1 < spt) ? nb : 0;  // the next input tile, issued at (c, 0) after A(s)
     } else {
-      allow = s + 1 < nst ? APW : 0;                  // A(s + 1)
+      allow = s + 1 < nst ? na : 0;                   // A(s + 1)
       if (ky == 2 && c + 1 < spt) allow += nb;        // + the next input tile, issued at (c, 1)
     }
     vm_wait(allow);
     __builtin_amdgcn_s_barrier();  // every wave's copies for stage s landed; stage s - 1's reads are done
     asm volatile("" ::: "memory");
+    if constexpr (TM) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      t_wait += t1 - t0;
+      t0 = t1;
+    }
     // this stage's copies (weights of stage s + AB - 1, and the next input tile at ky == AB - 2) are issued
     // one at a time between the MFMA groups below, where their issue cost hides under the matrix work
     const int sa = s + AB - 1;
@@ -152,13 +166,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
     h8* const bbw = bbase + ((c + 1) & 1) * BH8;
     auto piece = [&](int i) {
       if (i < APW) {
-        if (do_a) glds16(asrc[i] + (ca * 9 + kya * 3) * 64, abw + (wave + 4 * i) * 64);
+        if (do_a && wave + NW * i < AINS) glds16(asrc[i] + (ca * 9 + kya * 3) * 64, abw + (wave + NW * i) * 64);
       } else if (i < APW + BPW) {
         const int j = i - APW;
-        if (do_b && wave + 4 * j < BINS) {
+        if (do_b && wave + NW * j < BINS) {
           const void* src = boff[j] >= 0 ? static_cast<const void*>(xn + boff[j] + (c + 1) * 32)
                                          : static_cast<const void*>(g_zero_line);
-          glds16(src, bbw + (wave + 4 * j) * 64);
+          glds16(src, bbw + (wave + NW * j) * 64);
         }
       }
     };
@@ -191,25 +205,71 @@ __global__ __launch_bounds__(256, 2) void conv3x3_big_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int i = 12; i < APW + BPW; ++i) piece(i);  // stride 2: more copies than MFMA groups
+    if constexpr (TM) t_comp += __builtin_amdgcn_s_memtime() - t0;
+  }
+  if constexpr (TM) {
+    if (lane == 0 && blockIdx.x < 4096) {
+      unsigned long long* o = tm + (size_t(blockIdx.x) * 8 + wave) * 4;
+      o[0] = t_wait;
+      o[1] = t_comp;
+      o[2] = __builtin_amdgcn_s_memtime() - t_start;
+      o[3] = nst;
+    }
   }
   tile3_store<4, 4>(a, acc, n, oy0 + wr * 4, ox0, ct_blk + wc * 4, col, grp);
 }
 
-template <int S, int WM, int AB>
+static bool big3_timing() {
+  static const bool v = [] {
+    const char* e = getenv("FCE_BIG3_TIMING");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
+template <int S, int WM, int AB, int NW>
 static int launch_big3_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr size_t lds = Big3Geom<S, WM, AB>::lds;
+  constexpr size_t lds = Big3Geom<S, WM, AB, NW>::lds;
   if constexpr (lds <= 160 * 1024) {
-    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_big_kernel<S, WM, AB>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    static const bool big =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_big_kernel<S, WM, AB, NW, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_big_kernel<S, WM, AB, NW, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     if (!big) return fail(FCE_ERR_HIP, "conv 3x3 big tile: cannot opt in to >64 KiB LDS");
-    FCE_LAUNCH((conv3x3_big_kernel<S, WM, AB>), grid, dim3(256), lds, s, a);
+    if (!big3_timing()) {
+      FCE_LAUNCH((conv3x3_big_kernel<S, WM, AB, NW, false>), grid, dim3(NW * 64), lds, s, a, nullptr);
+      return FCE_OK;
+    }
+    // diagnostics: one timed launch, synchronised, summary on stderr
+    static unsigned long long* tm = nullptr;
+    const size_t nrec = size_t(4096) * 8 * 4;
+    if (!tm) FCE_HIP_CHECK(hipMalloc(&tm, nrec * 8));
+    FCE_HIP_CHECK(hipMemsetAsync(tm, 0, nrec * 8, s));
+    hipLaunchKernelGGL((conv3x3_big_kernel<S, WM, AB, NW, true>), grid, dim3(NW * 64), lds, s, a, tm);
+    FCE_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(nrec);
+    FCE_HIP_CHECK(hipMemcpy(h.data(), tm, nrec * 8, hipMemcpyDeviceToHost));
+    double w = 0, c = 0, t = 0;
+    int nw = 0, nst = 0;
+    for (size_t i = 0; i < nrec / 4; ++i)
+      if (h[i * 4 + 3]) {
+        w += h[i * 4];
+        c += h[i * 4 + 1];
+        t += h[i * 4 + 2];
+        nst = int(h[i * 4 + 3]);
+        ++nw;
+      }
+    if (nw)
+      fprintf(stderr, "big3<S%d,WM%d,AB%d,NW%d> waves %d stages %d: per stage wait %.0f compute %.0f clocks; lifetime %.0f\n",
+              S, WM, AB, NW, nw, nst, w / nw / nst, c / nw / nst, t / nw);
   }
   return FCE_OK;
 }
 
-int launch_big3(const ConvArgs& a, int wm, int ab, int stride, int n, hipStream_t s) {
-  FCE_CHECK(big3_ok(stride, wm, ab) && a.cin % 32 == 0 && a.up == 0, "conv 3x3 big tile: bad configuration");
-  const int th = (4 / wm) * 4;
+int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hipStream_t s) {
+  FCE_CHECK(big3_ok(stride, wm, ab, nw) && a.cin % 32 == 0 && a.up == 0, "conv 3x3 big tile: bad configuration");
+  const int th = (nw / wm) * 4;
   const int64_t tiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * n;
   ConvArgs b = a;
   b.gy = ((a.cout + 15) / 16 + wm * 4 - 1) / (wm * 4);
@@ -218,11 +278,11 @@ int launch_big3(const ConvArgs& a, int wm, int ab, int stride, int n, hipStream_
   int rc;
   if (stride == 1) {
     if (wm == 1)
-      rc = ab == 2 ? launch_big3_k<1, 1, 2>(b, grid, s) : launch_big3_k<1, 1, 3>(b, grid, s);
+      rc = ab == 2 ? launch_big3_k<1, 1, 2, 4>(b, grid, s) : launch_big3_k<1, 1, 3, 4>(b, grid, s);
     else
-      rc = ab == 2 ? launch_big3_k<1, 2, 2>(b, grid, s) : launch_big3_k<1, 2, 3>(b, grid, s);
+      rc = ab == 2 ? launch_big3_k<1, 2, 2, 4>(b, grid, s) : launch_big3_k<1, 2, 3, 4>(b, grid, s);
   } else {
-    rc = ab == 2 ? launch_big3_k<2, 2, 2>(b, grid, s) : launch_big3_k<2, 2, 3>(b, grid, s);
+    rc = ab == 2 ? launch_big3_k<2, 2, 2, 4>(b, grid, s) : launch_big3_k<2, 2, 3, 4>(b, grid, s);
   }
   if (rc != FCE_OK) return rc;
   return launch_status("conv3x3_big_kernel");

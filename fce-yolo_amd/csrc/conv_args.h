@@ -109,12 +109,12 @@ __device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP]
   }
 }
 
-// Big-tile LDS-DMA 3x3 configurations (conv3x3_big.hip), coded 0x800 | wm << 4 | (ab - 2) << 12: wm waves
-// along the couts, ab weight-stage buffers (stride 2 with wm 1 exceeds 160 KiB of LDS)
-static constexpr bool big3_ok(int s, int wm, int ab) {
-  return (ab == 2 || ab == 3) && (s == 1 ? (wm == 1 || wm == 2) : wm == 2);
+// Big-tile LDS-DMA 3x3 configurations (conv3x3_big.hip), coded 0x800 | wm << 4 | (ab - 2) << 12: wm waves along
+// the couts, ab weight-stage buffers, 4 waves per block (8-wave blocks were measured and dropped);
+// stride 2 needs wm 2 (LDS)
+static constexpr bool big3_ok(int s, int wm, int ab, int nw = 4) {
+  return nw == 4 && (ab == 2 || ab == 3) && (s == 1 ? (wm == 1 || wm == 2) : wm == 2);
 }
-
-int launch_big3(const ConvArgs& a, int wm, int ab, int stride, int n, hipStream_t s);
+int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hipStream_t s);
 
 }  // namespace fce
