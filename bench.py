@@ -175,6 +175,10 @@ def main():
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
     backend = os.environ.get("FCE_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
+    # FCE_DIST_FORCE=1 (rehearsal, under torch.distributed.run): the process group, the weight broadcast, the
+    # per-batch all-gather and the max-over-ranks timing run even with one rank
+    force = os.environ.get("FCE_DIST_FORCE") == "1" and "MASTER_ADDR" in os.environ
+    use_dist = world > 1 or force
     ndev = torch.cuda.device_count()
     if local >= ndev:
         if world > 1 and backend == "nccl":
@@ -182,20 +186,20 @@ def main():
         local = local % max(1, ndev)  # gloo rehearsal with more ranks than GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if use_dist:
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     model = DetectionModel(model_cfg(a.model))
     if rank == 0:
         model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
     model.eval().to(dev)
-    if world > 1:  # weights broadcast once per model load (RCCL over xGMI)
+    if use_dist:  # weights broadcast once per model load (RCCL over xGMI)
         broadcast_module(model, src=0)
 
     B, S = a.batch, a.imgsz
     # this rank's contiguous shard of a global batch of B * world images (dist.ShardedPredictor)
     sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")),
-                          lanes=a.lanes)
+                          lanes=a.lanes, gather=use_dist)
     eng = sp.engine
     for e in sp.pipe.engs:
         e.graph = bool(a.graph)
@@ -211,7 +215,7 @@ def main():
             sp.submit(x)
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()  # device-wide: includes the NMS side stream
 
@@ -228,7 +232,7 @@ def main():
     el = time.perf_counter() - t0
     _trace_marker()
     t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     ms_step = el / a.steps * 1e3
@@ -329,7 +333,7 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     sp.close()

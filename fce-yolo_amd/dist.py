@@ -123,10 +123,13 @@ class ShardedPredictor:
     overlaps the forward of batch i+1.  `results(k)` unpacks slot k in the unsharded image order."""
 
     def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, depth: int = 2,
-                 lanes: int = 1, **nms_kw):
+                 lanes: int = 1, gather: bool | None = None, **nms_kw):
+        """`gather` (default: world > 1) forces the collective path; with one rank it rehearses the RCCL
+        all-gather on the side stream (bench.py, FCE_DIST_FORCE=1)."""
         from .engine import NMS, Engine, Pipeline
 
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.do_gather = self.world > 1 if gather is None else bool(gather) and dist.is_initialized()
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         bs = batch_size or -(-total // self.world)
         self.sizes = shard_sizes(total, self.world, bs)
@@ -143,9 +146,9 @@ class ShardedPredictor:
         # each rank's packed outputs padded to bmax images, so every rank contributes the same bytes
         self.send = [torch.zeros(nb if self.batch < self.bmax else 0, dtype=torch.uint8, device=device)
                      for _ in range(depth)]
-        self.gathered = [torch.zeros(self.world * nb if self.world > 1 else 0, dtype=torch.uint8, device=device)
+        self.gathered = [torch.zeros(self.world * nb if self.do_gather else 0, dtype=torch.uint8, device=device)
                          for _ in range(depth)]
-        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.world > 1 else None, lanes=lanes, **nms_kw)
+        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.do_gather else None, lanes=lanes, **nms_kw)
 
     def _gather(self, k: int):
         from .engine import NMS
@@ -174,7 +177,7 @@ class ShardedPredictor:
         if k == self.pipe.pending:
             self.pipe.flush()
         self.pipe.nms_done[k].synchronize()
-        g = self.gathered[k] if self.world > 1 else self.pipe.nms[k].buf
+        g = self.gathered[k] if self.do_gather else self.pipe.nms[k].buf
         return unpack_gathered(g, self.sizes, self.max_det)
 
     def close(self):
