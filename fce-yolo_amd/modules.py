@@ -355,7 +355,10 @@ class C3k2(C2f):
     def _fused_desc(self, be, x):
         import os
 
-        if be.shape_only or os.environ.get("FCE_FUSE_C3K2", "0") == "0" or not hasattr(be, "c3k2"):
+        mode = os.environ.get("FCE_FUSE_C3K2", "0")  # "1": every qualifying block; a number N > 1: h * w <= N
+        if be.shape_only or mode == "0" or not hasattr(be, "c3k2"):
+            return None
+        if mode != "1" and x.h * x.w > int(mode):
             return None
         if len(self.m) != 1 or type(self.m[0]) is not Bottleneck or not self.m[0].add:
             return None
