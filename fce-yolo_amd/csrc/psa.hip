@@ -22,16 +22,31 @@ namespace fce {
 int dwconv3x3(const fce_tensor& x, int stride, const float* w, int wcs, const float* bias, int act,
               const fce_tensor& y, hipStream_t s, int variant = -1);
 
+// XCD-aware block order: the grid is 1-D, block b runs on XCD b % 8, and all QT query tiles of one (image, head)
+// pair get blocks on the same XCD (pair p on XCD p % 8), so that pair's K / V lines are fetched into one L2
+// instead of up to QT of them.  Blocks past the last pair exit at once.
+__device__ __forceinline__ bool psa_block(int QT, int P, int heads, int& qt, int& n, int& hd) {
+  const int b = int(blockIdx.x), xcd = b & 7, slot = b >> 3;
+  const int pl = slot / QT;
+  qt = slot - pl * QT;
+  const int pair = pl * 8 + xcd;
+  if (pair >= P) return false;
+  n = pair / heads;
+  hd = pair - n * heads;
+  return true;
+}
+
 template <int KD, int HD>
 __global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
-                                                                 int ycs, float scale_log2) {
+                                                                 int ycs, float scale_log2, int QT, int P, int heads) {
   static_assert(KD == 32 && HD == 64, "C2PSA geometry");
   constexpr int KT = 64, VTS = KT + 4;  // key tile, padded LDS row (conflict-free 8-byte reads)
   __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VTS];
-  const int n = blockIdx.z, hd = blockIdx.y;
+  int qt, n, hd;
+  if (!psa_block(QT, P, heads, qt, n, hd)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
-  const int q = blockIdx.x * 64 + wave * 16 + col;
+  const int q = qt * 64 + wave * 16 + col;
   const _Float16* base = qkv + int64_t(n) * N * qcs + hd * (2 * KD + HD);
   // B operand Q^T: lane holds Q[q][8g..8g+7]
   h8 qf = h8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -133,15 +148,17 @@ __global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16*
 // order over 64-key tiles: bitwise-identical results.
 template <int KD, int HD>
 __global__ __launch_bounds__(256) void psa_attention_chunk_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
-                                                                  int ycs, float scale_log2) {
+                                                                  int ycs, float scale_log2, int QT, int P,
+                                                                  int heads) {
   static_assert(KD == 32 && HD == 64, "C2PSA geometry");
   constexpr int KT = 64, KC = 256, VTS = KC + 4;
   __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VTS];
   __shared__ __attribute__((aligned(16))) h8 kl[KC * 4];  // [key][4 x 8 dims], piece g at g ^ ((key >> 1) & 3)
-  const int n = blockIdx.z, hd = blockIdx.y;
+  int qt, n, hd;
+  if (!psa_block(QT, P, heads, qt, n, hd)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
-  const int q = blockIdx.x * 64 + wave * 16 + col;
+  const int q = qt * 64 + wave * 16 + col;
   const _Float16* base = qkv + int64_t(n) * N * qcs + hd * (2 * KD + HD);
   h8 qf = h8{0, 0, 0, 0, 0, 0, 0, 0};
   if (q < N) qf = *reinterpret_cast<const h8*>(base + int64_t(q) * qcs + 8 * g);
@@ -277,7 +294,9 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
     const int st = dwconv3x3(vx, 1, pe_w + h * head_dim, heads * head_dim, pe_b + h * head_dim, 0, vy, s);
     if (st) return st;
   }
-  dim3 grid((N + 63) / 64, heads, qkv.n);
+  const int QT = (N + 63) / 64, P = heads * qkv.n;
+  FCE_CHECK(int64_t(8) * ((P + 7) / 8) * QT < (int64_t(1) << 31), "psa_attention: grid too large");
+  const dim3 grid(unsigned(8 * ((P + 7) / 8) * QT));
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)key_dim);
   static const bool tiled = [] {  // diagnostics: FCE_PSA_TILED=1 runs the per-64-key-tile kernel
     const char* e = getenv("FCE_PSA_TILED");
@@ -286,12 +305,12 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
   if (tiled) {
     FCE_LAUNCH((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
                static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
-               static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
+               static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2, QT, P, heads);
     return launch_status("psa_attention_mfma_kernel");
   }
   FCE_LAUNCH((psa_attention_chunk_kernel<32, 64>), grid, dim3(256), 0, s,
              static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
-             static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2);
+             static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2, QT, P, heads);
   return launch_status("psa_attention_chunk_kernel");
 }
 
