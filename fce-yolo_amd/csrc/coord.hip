@@ -138,14 +138,28 @@ __device__ __forceinline__ void pool_cols(const _Float16* x, int xcs, int H, int
   }
 }
 
-// both poolings in one launch (grid (H + column strips, N)): blocks [0, H) take a row each, the rest a
-// strip of XW columns; the two halves read disjoint work and run side by side
+// both poolings in one launch: per image H row blocks (a row each) then the column-strip blocks (XW columns
+// each).  The 1-D grid is XCD-aware: block b runs on XCD b % 8, and all blocks of image n sit on XCD n % 8 in
+// that order, so an image's column strips re-read its rows from the L2 that the row blocks just filled
+// instead of from another XCD's fabric path.  Blocks past the last image exit at once.  Below 8 images
+// (aff = 0) the blocks of an image spread over every XCD instead, so a small batch still uses the whole chip.
 __global__ __launch_bounds__(256) void pool_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xh,
-                                                   float* xw) {
-  if (int(blockIdx.x) < H)
-    pool_rows(x, xcs, H, W, C, xh, blockIdx.x, blockIdx.y);
+                                                   float* xw, int N, int BPI, int aff) {
+  const int b = int(blockIdx.x);
+  int n, j;
+  if (aff) {
+    const int xcd = b & 7, slot = b >> 3, il = slot / BPI;
+    j = slot - il * BPI;
+    n = il * 8 + xcd;
+  } else {
+    n = b / BPI;
+    j = b - n * BPI;
+  }
+  if (n >= N) return;
+  if (j < H)
+    pool_rows(x, xcs, H, W, C, xh, j, n);
   else
-    pool_cols(x, xcs, H, W, C, xw, blockIdx.x - H, blockIdx.y);
+    pool_cols(x, xcs, H, W, C, xw, j - H, n);
 }
 
 // ---------------------------------------------------------------------------- 2. projections
@@ -1015,7 +1029,11 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   int RG = 1;  // pool_col_groups on the host
   while (RG < 8 && (C / 8) * RG * 2 <= 256 && H >= 16 * RG) RG *= 2;
   const int XW = 256 / ((C / 8) * RG);
-  FCE_LAUNCH(pool_kernel, dim3(H + (W + XW - 1) / XW, N), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.xw);
+  const int BPI = H + (W + XW - 1) / XW;
+  const int aff = N >= 8;
+  const int64_t nblk = int64_t(aff ? 8 * ((N + 7) / 8) : N) * BPI;
+  FCE_CHECK(nblk < (int64_t(1) << 31), "coord pooling: grid too large");
+  FCE_LAUNCH(pool_kernel, dim3(unsigned(nblk)), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.xw, N, BPI, aff);
   int st = launch_status("coord pooling");
   if (st) return st;
   const char* nc = getenv("FCE_COORD_NO_CORE");  // diagnostics: force the split projection / attention path
