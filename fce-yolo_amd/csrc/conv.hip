@@ -1558,6 +1558,16 @@ struct DwArgs {
   int act;
 };
 
+// XCD-aware 2-D block order: block b runs on XCD b % 8; logical block L = (b % 8) * per + b / 8 gives each
+// XCD a contiguous run of (x fastest, then y) blocks, so the row bands that share halo rows meet in one L2
+__device__ __forceinline__ void xcd_block2(int& bx, int& by) {
+  const int gx = int(gridDim.x), total = gx * int(gridDim.y), b = int(blockIdx.y) * gx + int(blockIdx.x);
+  const int per = total >> 3, body = per << 3;
+  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+  by = L / gx;
+  bx = L - by * gx;
+}
+
 // One thread = PX adjacent output pixels x 8 channels: the 9 tap weights are loaded once and the
 // S*(PX-1)+3 input columns of each row are shared by the PX outputs.
 template <int S, int PX>
@@ -1565,10 +1575,12 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
   constexpr int NCOL = S * (PX - 1) + 3;
   const int cg8 = a.C >> 3;
   const int Q = (a.Wo + PX - 1) / PX;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
+  int bx, by;
+  xcd_block2(bx, by);  // the rows that share input rows run on one XCD's L2
+  const int idx = bx * 256 + threadIdx.x;
   if (idx >= Q * cg8) return;
   const int q = idx / cg8, c0 = (idx - q * cg8) * 8;
-  const int row = blockIdx.y, n = row / a.Ho, oy = row - n * a.Ho;
+  const int row = by, n = row / a.Ho, oy = row - n * a.Ho;
   const int ox0 = q * PX, ix0 = ox0 * S - 1;
   float wk[9][8];
 #pragma unroll
@@ -1630,9 +1642,11 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
 template <int S>
 __global__ __launch_bounds__(256) void dwconv_rows_kernel(DwArgs a, int CS) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
-  const int c0 = blockIdx.x * CS;
+  int bx, by;
+  xcd_block2(bx, by);
+  const int c0 = bx * CS;
   const int cs = min(CS, a.C - c0), cg = cs >> 3;
-  const int row = blockIdx.y, n = row / a.Ho, oy = row - n * a.Ho;
+  const int row = by, n = row / a.Ho, oy = row - n * a.Ho;
   float* wl = dsm;              // [9][CS]
   float* bl = wl + 9 * CS;      // [CS]
   h8* rows = reinterpret_cast<h8*>(bl + CS);  // [3][W][CS/8]
@@ -1743,16 +1757,6 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
 // lines); each thread computes PY outputs down its column from (PY-1)*S+3 input rows, every loaded
 // row feeding all the outputs that use it.  Out-of-image taps are skipped (selects, no branches) and
 // each output accumulates its taps in (ky, kx) order with fmaf, like the other variants.
-// XCD-aware 2-D block order: block b runs on XCD b % 8; logical block L = (b % 8) * per + b / 8 gives each
-// XCD a contiguous run of (x fastest, then y) blocks, so the row bands that share halo rows meet in one L2
-__device__ __forceinline__ void xcd_block2(int& bx, int& by) {
-  const int gx = int(gridDim.x), total = gx * int(gridDim.y), b = int(blockIdx.y) * gx + int(blockIdx.x);
-  const int per = total >> 3, body = per << 3;
-  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
-  by = L / gx;
-  bx = L - by * gx;
-}
-
 template <int S, int PY>
 __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
   const int cg = a.C >> 3;
