@@ -339,6 +339,35 @@ def test_nms_large_candidate_set_global_sort(device):
 
 
 
+@pytest.mark.parametrize("case", ["group_done", "group_runs_out", "group_is_everything"])
+def test_nms_equal_top_score_group(case, device):
+    """>= max_det candidates share the top score (saturated sigmoids): ties resolved by anchor order, whether the
+    greedy stops inside the tied group, runs through it (one pile of near-identical boxes), or the whole candidate
+    set is tied.  Bit-exact vs the oracle."""
+    rng = np.random.default_rng({"group_done": 7, "group_runs_out": 8, "group_is_everything": 9}[case])
+    A, nc = 6000, 4
+    p = np.zeros((2, 4 + nc, A), np.float32)
+    for b in range(2):
+        p[b, 0:2] = rng.random((2, A)) * 600 + 20
+        p[b, 2:4] = rng.random((2, A)) * 40 + 8
+        cls = rng.integers(0, nc, A)
+        sc = (0.3 + 0.6 * rng.random(A)).astype(np.float32)
+        top = rng.choice(A, {"group_done": 2000, "group_runs_out": 700, "group_is_everything": A}[case], replace=False)
+        sc[top] = 1.0
+        if case == "group_runs_out":  # the top group is one pile of near-identical boxes: almost all suppressed
+            p[b, 0, top], p[b, 1, top] = 300 + rng.random(len(top)), 300 + rng.random(len(top))
+            p[b, 2, top], p[b, 3, top] = 50, 50
+            cls[top] = 0
+        p[b, 4 + cls, np.arange(A)] = sc
+    pt = torch.from_numpy(p).to(device)
+    for max_det in (300, 100):
+        dets, keep = non_max_suppression(pt, 0.25, 0.7, max_det, return_idxs=True)
+        od, ok = nms_oracle.non_max_suppression(p, 0.25, 0.7, max_det)
+        for b in range(2):
+            assert np.array_equal(keep[b].cpu().numpy(), ok[b]), (b, max_det)
+            assert np.array_equal(dets[b].cpu().numpy(), od[b]), (b, max_det)
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_nms_clustered_suppression_chains(seed, device):
     """Heavy, chained suppression: jittered boxes around a few centres, few classes, tied (quantised)
