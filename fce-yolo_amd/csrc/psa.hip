@@ -3,8 +3,8 @@
 // with pe = depthwise 3x3 (BN folded, no act) over v viewed as (B, heads*hd, H, W).
 // qkv is the NHWC fp16 output of the qkv 1x1 conv: channel (head*(2kd+hd) + r) is row r of that head.
 //
-// pe(v) runs first through the depthwise-conv kernel (one launch per head on the v channel slice),
-// writing y; the attention kernel then adds its output into y.
+// pe(v) is computed in the attention kernel's epilogue for each query pixel, with the depthwise kernel's exact
+// arithmetic (the diagnostic per-64-key-tile kernel still takes it from a depthwise pass per head).
 //
 // Attention = flash-style on MFMA (v_mfma_f32_16x16x32_f16), one block = (image, head, 64 queries),
 // one wave = 16 queries, K/V streamed in 64-key tiles:
@@ -149,7 +149,8 @@ __global__ __launch_bounds__(256) void psa_attention_mfma_kernel(const _Float16*
 template <int KD, int HD>
 __global__ __launch_bounds__(256) void psa_attention_chunk_kernel(const _Float16* qkv, int qcs, int N, _Float16* y,
                                                                   int ycs, float scale_log2, int QT, int P,
-                                                                  int heads) {
+                                                                  int heads, int H, int W, const float* pe_w,
+                                                                  const float* pe_b) {
   static_assert(KD == 32 && HD == 64, "C2PSA geometry");
   constexpr int KT = 64, KC = 256, VTS = KC + 4;
   __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VTS];
@@ -260,13 +261,38 @@ __global__ __launch_bounds__(256) void psa_attention_chunk_kernel(const _Float16
   if (q >= N) return;
   const float inv = 1.0f / l;
   _Float16* yo = y + (int64_t(n) * N + q) * ycs + hd * HD;
+  // pe(v) of this query's pixel, computed here exactly as the depthwise kernel does it (bias, then the taps in
+  // (ky, kx) order with fmaf, rows outside the image skipped, columns outside read as zero, fp16 rounding): the
+  // separate per-head depthwise launches and the y round trip they needed are gone, results unchanged
+  const int py = q / W, px = q - py * W;
+  const int wcs = heads * HD;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    _Float16* p = yo + 16 * dt + 4 * g;
-    const h4 pe = *reinterpret_cast<const h4*>(p);  // pe(v) written by the depthwise pass
+    const int d0 = 16 * dt + 4 * g;
+    const f4 bb = *reinterpret_cast<const f4*>(pe_b + hd * HD + d0);
+    float pa[4] = {bb[0], bb[1], bb[2], bb[3]};
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = py - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = px - 1 + kx;
+        const h4 v = (ix >= 0 && ix < W)
+                         ? *reinterpret_cast<const h4*>(base + int64_t(iy * W + ix) * qcs + 2 * KD + d0)
+                         : h4{0, 0, 0, 0};
+        const f4 wk = *reinterpret_cast<const f4*>(pe_w + (ky * 3 + kx) * wcs + hd * HD + d0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pa[j] = __builtin_fmaf((float)v[j], wk[j], pa[j]);
+      }
+    }
+    _Float16* p = yo + d0;
     h4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = (_Float16)((float)pe[j] + acc[dt][j] * inv);
+    for (int j = 0; j < 4; ++j) {
+      const _Float16 pe = (_Float16)fpin(pa[j]);
+      o[j] = (_Float16)((float)pe + acc[dt][j] * inv);
+    }
     *reinterpret_cast<h4*>(p) = o;
   }
 }
@@ -283,8 +309,13 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
     return fail(FCE_ERR_UNSUPPORTED, "psa_attention: only key_dim 32 / head_dim 64 (C2PSA, num_heads = c // 64)");
   const int N = qkv.h * qkv.w;
   if (N == 0 || qkv.n == 0) return FCE_OK;
-  // pe(v): depthwise 3x3 on each head's v slice -> y slice (the attention kernel accumulates on top)
-  for (int h = 0; h < heads; ++h) {
+  static const bool tiled = [] {  // diagnostics: FCE_PSA_TILED=1 runs the per-64-key-tile kernel
+    const char* e = getenv("FCE_PSA_TILED");
+    return e && atoi(e) != 0;
+  }();
+  // pe(v) for the diagnostic tiled kernel: depthwise 3x3 on each head's v slice -> y slice (the kernel adds on
+  // top); the default chunk kernel computes pe itself in its epilogue
+  for (int h = 0; tiled && h < heads; ++h) {
     fce_tensor vx = qkv;
     vx.c = head_dim;
     vx.coff = qkv.coff + h * (2 * key_dim + head_dim) + 2 * key_dim;
@@ -298,10 +329,6 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
   FCE_CHECK(int64_t(8) * ((P + 7) / 8) * QT < (int64_t(1) << 31), "psa_attention: grid too large");
   const dim3 grid(unsigned(8 * ((P + 7) / 8) * QT));
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)key_dim);
-  static const bool tiled = [] {  // diagnostics: FCE_PSA_TILED=1 runs the per-64-key-tile kernel
-    const char* e = getenv("FCE_PSA_TILED");
-    return e && atoi(e) != 0;
-  }();
   if (tiled) {
     FCE_LAUNCH((psa_attention_mfma_kernel<32, 64>), grid, dim3(256), 0, s,
                static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
@@ -310,7 +337,7 @@ int psa_attention(const fce_tensor& qkv, int heads, int key_dim, int head_dim, c
   }
   FCE_LAUNCH((psa_attention_chunk_kernel<32, 64>), grid, dim3(256), 0, s,
              static_cast<const _Float16*>(qkv.data) + qkv.coff, qkv.cstride, N,
-             static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2, QT, P, heads);
+             static_cast<_Float16*>(y.data) + y.coff, y.cstride, scale_log2, QT, P, heads, qkv.h, qkv.w, pe_w, pe_b);
   return launch_status("psa_attention_chunk_kernel");
 }
 
