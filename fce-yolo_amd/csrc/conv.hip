@@ -2144,9 +2144,9 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
 // gathering the 8 (ci, ky, kx) values of its lane group from LDS and runs RC MFMAs (16 couts each).
 // Lane (col, grp) of D holds couts 4 grp .. of pixel col: 8-byte stores, a fragment's 16 pixels x
 // RC*16 couts contiguous in NHWC.  fp16 weights, fp32 accumulation, like every other conv here.
-template <typename T, int RC>
+template <typename T, int RC, int SR>
 __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float16* wfr) {
-  constexpr int SR = 4;                 // output rows per block
+  // SR output rows per block
   constexpr int IR = 2 * SR + 1;        // staged input rows
   extern __shared__ __attribute__((aligned(16))) _Float16 ssm[];  // [C][IR][8 + W + 8]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2623,20 +2623,37 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     const int PX = coutT <= 32 ? 2 : 1;  // measured: PX 2 beats 4 (occupancy) and 1 (reuse) at cout 16
     const char* sv = getenv("FCE_STEM_VALU");  // diagnostics: the fp32 VALU stem instead of MFMA
     // the staged rows exceed 64 KiB above W = 1168 (imgsz 1280: 70 KiB): gfx950 LDS opt-in up to 160 KiB
+    static const int SRE = [] {  // output rows per block (FCE_STEM_SR = 2 / 4 / 8; measured default 4)
+      const char* e = getenv("FCE_STEM_SR");
+      const int v = e ? atoi(e) : 4;
+      return v == 2 || v == 8 ? v : 4;
+    }();
+    int SR = SRE;
+    if (size_t(x.c) * (2 * SR + 1) * (x.w + 16) * 2 + 16 > 160 * 1024) SR = 4;
     if (stem_mfma_ok(d) && d.stride == 2 && x.c == d.cin && d.cout % 16 == 0 && x.w % 8 == 0 &&
-        size_t(x.c) * 9 * (x.w + 16) * 2 + 16 <= 160 * 1024 && !(sv && atoi(sv))) {
-      const size_t lds = size_t(x.c) * 9 * (x.w + 16) * sizeof(_Float16) + 16;  // + the dummy staging slot
-      const int64_t blocks2 = int64_t(x.n) * ((Ho + 3) / 4);
+        size_t(x.c) * (2 * SR + 1) * (x.w + 16) * 2 + 16 <= 160 * 1024 && !(sv && atoi(sv))) {
+      // + the dummy staging slot
+      const size_t lds = size_t(x.c) * (2 * SR + 1) * (x.w + 16) * sizeof(_Float16) + 16;
+      const int64_t blocks2 = int64_t(x.n) * ((Ho + SR - 1) / SR);
       FCE_CHECK(blocks2 < (int64_t(1) << 31), "stem conv: input too large");
       const _Float16* wfr = reinterpret_cast<const _Float16*>(static_cast<const char*>(w) + stem_fp32_bytes(d));
       const int rc = d.cout / 16;
-#define STEMM(T, RC)                                                                                          \
+#define STEMM_SR(T, RC, SRC)                                                                                  \
   do {                                                                                                        \
-    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_mfma_kernel<T, RC>),     \
+    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_mfma_kernel<T, RC, SRC>), \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==    \
                             hipSuccess;                                                                       \
     if (!big && lds > 64 * 1024) return fail(FCE_ERR_HIP, "stem conv: cannot opt in to >64 KiB LDS");        \
-    FCE_LAUNCH((stem_mfma_kernel<T, RC>), dim3(unsigned(blocks2)), dim3(256), lds, s, a, wfr);                \
+    FCE_LAUNCH((stem_mfma_kernel<T, RC, SRC>), dim3(unsigned(blocks2)), dim3(256), lds, s, a, wfr);           \
+  } while (0)
+#define STEMM(T, RC)          \
+  do {                        \
+    if (SR == 2)              \
+      STEMM_SR(T, RC, 2);     \
+    else if (SR == 8)         \
+      STEMM_SR(T, RC, 8);     \
+    else                      \
+      STEMM_SR(T, RC, 4);     \
   } while (0)
 #define STEMM_T(T)          \
   do {                      \
@@ -2657,6 +2674,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
         STEMM_T(uint8_t);
 #undef STEMM_T
 #undef STEMM
+#undef STEMM_SR
       return launch_status("stem_mfma_kernel");
     }
     if (d.k == 3 && d.stride == 2 && x.c == 3 && x.w % (2 * PX) == 0) {
