@@ -6,7 +6,7 @@
 
 A step = one global batch of B images per GPU through `dist.ShardedPredictor`: each rank's contiguous
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
-per rank) runs the whole forward (direct launches; --graph 1 for hipGraph replay) + the device NMS, and
+per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
 with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
 default three batches are in flight per GPU (--lanes 3, engine.Pipeline lanes): three executors with their
 own arenas on three streams, each running forward then NMS of every third batch, so one batch's
@@ -79,14 +79,18 @@ def parse_args():
     ap.add_argument("--sequential", action="store_true", help="forward then NMS on one stream (no overlap)")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("FCE_LANES", "3")),
                     help="batches in flight per GPU (engine.Pipeline lanes: one executor + stream each)")
-    ap.add_argument("--graph", type=int, default=0, help="1: replay a captured hipGraph; 0: direct launches "
-                    "(measured faster on ROCm 7.2, DESIGN.md)")
+    ap.add_argument("--graph", type=int, default=-1, help="1: replay a captured hipGraph per lane; 0: direct "
+                    "launches; -1 (default): replay when lanes > 1 (ties direct launches there, 28.2k both; with one "
+                    "lane direct launches are faster, DESIGN.md)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     ap.add_argument("--profile-passes", type=int, default=10, help="per-op HIP-event passes averaged")
     ap.add_argument("--predict-steps", type=int, default=10,
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.graph < 0:
+        a.graph = 1 if a.lanes > 1 else 0
+    return a
 
 
 def model_cfg(name: str):
@@ -311,7 +315,8 @@ def main():
         "data": "synthetic torch.rand(B,3,S,S) fp16 per rank; seeded random-init weights of the architecture",
         "config": {"workload": f"{stem} detection inference (forward + decode + NMS) @ {S}x{S}, {B} images/GPU",
                    "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}",
-                   "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes},
+                   "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes,
+                   "forward_launch": "hipgraph" if a.graph else "direct"},
         "roofline": roof,
         "forward_ms_per_batch": round(fwd_ms, 4),
         "forward_kernel_busy_ms": round(kernel_ms, 4),
