@@ -2378,8 +2378,8 @@ static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (rin
 int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap) {
   if (is_stem(d)) return 0;
   if (is_dw(d)) {  // depthwise kernel variants, coded 100 + variant
-    int v[4];
-    const int nv = d.k == 3 ? dwconv_variants(d.cin, in_w, v, 4) : 0;
+    int v[8];  // every variant dwconv_variants lists (a cap of 4 used to drop the 4-row column runs)
+    const int nv = d.k == 3 ? dwconv_variants(d.cin, in_w, v, 8) : 0;
     for (int i = 0; i < nv && i < cap; ++i) out[i] = 100 + v[i];
     return std::min(nv, cap);
   }
