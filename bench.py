@@ -4,6 +4,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) launches the N ranks itself: before
+torch is even imported, it runs the torch.distributed.run command above as a child process (one rank per
+GPU, 127.0.0.1, a free port) and exits with its status -- the reference's trainer does the same with its
+generated DDP command (engine/trainer.py:233-236, utils/dist.py:77-104).  The parent never touches the GPU.
+A rank whose WORLD_SIZE differs from --gpus fails with a non-zero status.
+
 A step = one global batch of B images per GPU through `dist.ShardedPredictor`: each rank's contiguous
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
@@ -22,12 +28,39 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 from collections import defaultdict
 from pathlib import Path
 
-import torch
+
+def launch_command(argv, env):
+    """The torch.distributed.run command that starts `--gpus N` ranks of this script, or None when this
+    process is already a rank (WORLD_SIZE set) or N == 1.  Pure: no torch import, no GPU call."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    a, _ = pre.parse_known_args(argv)
+    if a.gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+if __name__ == "__main__":
+    _cmd = launch_command(sys.argv[1:], os.environ)
+    if _cmd is not None:  # launcher: start the ranks as a child process (never exec), exit with its status
+        if os.environ.get("FCE_BENCH_DRY_LAUNCH") == "1":
+            print(json.dumps({"launch": _cmd, "torch_imported": "torch" in sys.modules}), flush=True)
+            sys.exit(0)
+        import subprocess
+
+        sys.exit(subprocess.call(_cmd))
+
+import torch  # noqa: E402
 import torch.distributed as dist
 
 ROOT = Path(__file__).resolve().parent
@@ -177,7 +210,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != a.gpus:
-        a.gpus = world if world > 1 else a.gpus
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}: one rank per GPU "
+                         f"(run `python bench.py --gpus {a.gpus}` or torch.distributed.run --nproc-per-node {a.gpus})")
     backend = os.environ.get("FCE_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
     # FCE_DIST_FORCE=1 (rehearsal, under torch.distributed.run): the process group, the weight broadcast, the
     # per-batch all-gather and the max-over-ranks timing run even with one rank
@@ -192,6 +226,8 @@ def main():
     dev = torch.device("cuda", local)
     if use_dist:
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group world size {dist.get_world_size()} != WORLD_SIZE {world}")
 
     model = DetectionModel(model_cfg(a.model))
     if rank == 0:
@@ -251,6 +287,22 @@ def main():
     barrier()
     fwd_ms = (time.perf_counter() - t1) / a.steps * 1e3
 
+    # strictly one batch at a time: forward (direct launches, the faster mode with one batch in flight) then
+    # NMS, host-synchronised after every batch -> the one-lane rate and the per-batch latency (submit ->
+    # detections ready); max over ranks
+    lat = []
+    for _ in range(max(5, min(a.steps, 30))):
+        t2 = time.perf_counter()
+        pr = eng(x, graph=False)
+        if not a.no_nms:
+            nms(pr, eng.best)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t2)
+    lat_t = torch.tensor([sum(lat) / len(lat), sorted(lat)[len(lat) // 2]], dtype=torch.float64, device=dev)
+    if use_dist:
+        dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
+    lat_mean, lat_med = (float(v) for v in lat_t.tolist())
+
     # per-op HIP-event profile (events on the launching stream around every op of the same direct-launch
     # sequence, averaged over `steps` passes) -> dominant kernel family roofline
     _trace_marker()
@@ -300,6 +352,11 @@ def main():
     kernel_ms = sum(p[3] for p in prof)
     stem = Path(a.model).stem
     batch_flops = sum(p[2] for p in prof)  # 2*MAC of every conv / matmul of one batch (op_cost)
+    batch_bytes = sum(p[1] for p in prof)  # algorithmic bytes of every op of one batch (op_cost)
+    # whole-forward roofline: achieved = img/s x GFLOP/img against min(MFMA peak, AI x HBM peak)
+    ai_fwd = batch_flops / max(batch_bytes, 1.0)
+    roof_tfs = min(MFMA_F16_PEAK_TFS, ai_fwd * HBM_PEAK_GBS / 1e3)
+    ach_tfs = value / world * batch_flops / B / 1e12
     out = {
         "metric": "images/sec/GPU @ 640x640 bs=32, yolo11n-fce; fraction of fp16 MFMA roofline",
         "value": round(value, 2),
@@ -318,6 +375,14 @@ def main():
                    "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes,
                    "forward_launch": "hipgraph" if a.graph else "direct"},
         "roofline": roof,
+        "roofline_forward": {"achieved": round(ach_tfs, 3), "peak": round(roof_tfs, 2), "unit": "TFLOP/s",
+                             "frac": round(ach_tfs / roof_tfs, 4), "ai_flop_per_byte": round(ai_fwd, 2),
+                             "bound": "mfma" if ai_fwd >= RIDGE else "hbm",
+                             "source": "img/s x algorithmic flop/img over min(2.5 PF, AI x 8 TB/s), AI = op_cost flops "
+                                       "/ op_cost bytes of the whole forward (BASELINE.md §3)"},
+        "value_1lane": round(B * world / lat_mean, 2),
+        "latency_ms_per_batch": {"mean": round(lat_mean * 1e3, 4), "median": round(lat_med * 1e3, 4),
+                                 "mode": "one batch at a time: forward (direct launches) + NMS, host sync per batch"},
         "forward_ms_per_batch": round(fwd_ms, 4),
         "forward_kernel_busy_ms": round(kernel_ms, 4),
         "profile_passes": max(1, a.profile_passes),
@@ -336,6 +401,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds, B)
     elif rank == 0:
         out["cpu_baseline"] = None
+    out["process_group"] = ({"backend": dist.get_backend(), "world_size": dist.get_world_size()} if use_dist
+                            else None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_dist:

@@ -17,6 +17,7 @@ F16, F32, U8 = 0, 1, 2
 NHWC, NCHW = 0, 1
 ACT_NONE, ACT_SILU = 0, 1
 EPI_STORE, EPI_WSTORE, EPI_ACCUM = 0, 1, 2
+PLAN_NO_AUTOTUNE = 1
 
 
 class FceError(RuntimeError):
@@ -154,6 +155,7 @@ _SIGS = {
     "fce_net_add_detect": (_I, [_P, _I, _P, _P, _I]),
     "fce_net_add_conv_detect": (_I, [_P, _PCD, _I, _I, _I, _I, C.c_float, _I, _I, _P, _P]),
     "fce_net_plan": (_I, [_P, _I, _I, _I]),
+    "fce_net_plan_ex": (_I, [_P, _I, _I, _I, _I]),
     "fce_net_arena_bytes": (_SZ, [_P]),
     "fce_net_num_anchors": (_I, [_P]),
     "fce_net_forward": (_I, [_P, _PT, _P, _I, _P]),

@@ -861,7 +861,13 @@ static int autotune(fce_net* net) {
 }
 
 int fce_net_plan(fce_net* net, int batch, int h, int w) {
+  const char* at = getenv("FCE_AUTOTUNE");
+  return fce_net_plan_ex(net, batch, h, w, (at && atoi(at) == 0) ? FCE_PLAN_NO_AUTOTUNE : 0);
+}
+
+int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags) {
   FCE_CHECK(net && batch > 0 && h > 0 && w > 0, "fce_net_plan: bad argument");
+  FCE_CHECK((flags & ~FCE_PLAN_NO_AUTOTUNE) == 0, "fce_net_plan_ex: unknown flags");
   FCE_CHECK(h % 32 == 0 && w % 32 == 0, "fce_net_plan: H and W must be multiples of 32 (max stride)");
   FCE_GUARD({
     net->release();
@@ -903,8 +909,8 @@ int fce_net_plan(fce_net* net, int batch, int h, int w) {
     FCE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&net->arena), std::max<size_t>(off, 256)));
     FCE_HIP_CHECK(hipMalloc(&net->ws, ws));
     FCE_HIP_CHECK(hipMemset(net->arena, 0, std::max<size_t>(off, 256)));
-    const char* at = getenv("FCE_AUTOTUNE");
-    if (!at || atoi(at) != 0) return autotune(net);
+    net->cur_best = nullptr;
+    if (!(flags & FCE_PLAN_NO_AUTOTUNE)) return autotune(net);
     return FCE_OK;
   })
 }
@@ -924,10 +930,22 @@ int fce_net_forward(fce_net* net, const fce_tensor* input, float* pred, int grap
   return fce_net_forward_best(net, input, pred, nullptr, graph, stream);
 }
 
+static int forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
+                        void* stream);
+
 int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
                          void* stream) {
   FCE_CHECK(net && pred, "fce_net_forward: null argument");
+  // the Detect epilogues read cur_best while this call enqueues (captured graphs hold it by value); it is
+  // cleared afterwards so a later profile / autotune pass can never write into a caller's key buffer
   net->cur_best = best;
+  const int st = forward_best(net, input, pred, best, graph, stream);
+  net->cur_best = nullptr;
+  return st;
+}
+
+static int forward_best(fce_net* net, const fce_tensor* input, float* pred, unsigned long long* best, int graph,
+                        void* stream) {
   int st = check_input(net, input);
   if (st) return st;
   hipStream_t caller = S(stream);
@@ -999,6 +1017,7 @@ int fce_net_forward_best(fce_net* net, const fce_tensor* input, float* pred, uns
 int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int* launches, int cap,
                     void* stream) {
   FCE_CHECK(net && pred && ms, "fce_net_profile: null argument");
+  net->cur_best = nullptr;  // no best-class keys: the Detect epilogues write pred only
   int st = check_input(net, input);
   if (st) return st;
   hipStream_t s = S(stream);

@@ -135,8 +135,9 @@ class ShardedPredictor:
         self.sizes = shard_sizes(total, self.world, bs)
         self.start, self.end = shard_range(total, self.world, self.rank, bs)
         self.batch = self.end - self.start
-        if self.batch <= 0:
-            raise ValueError(f"rank {self.rank}: empty shard of a {total}-image batch over {self.world} ranks")
+        if min(self.sizes) <= 0:  # decided from sizes every rank computes alike: all ranks raise, none hangs
+            raise ValueError(f"empty shard(s) {self.sizes} of a {total}-image batch over {self.world} ranks "
+                             f"(batch_size {bs}): every rank needs at least one image")
         self.bmax = max(self.sizes)
         self.engine = Engine(model, self.batch, imgsz, device)
         self.max_det = nms_kw.get("max_det", 300)
@@ -173,12 +174,15 @@ class ShardedPredictor:
         self.pipe.flush()
 
     def results(self, k: int):
-        """(dets, keep) per image of the whole global batch, in the unsharded order."""
+        """(dets, keep) per image of the whole global batch, in the unsharded order (with gather=False: this
+        rank's shard only)."""
         if k == self.pipe.pending:
             self.pipe.flush()
         self.pipe.nms_done[k].synchronize()
-        g = self.gathered[k] if self.do_gather else self.pipe.nms[k].buf
-        return unpack_gathered(g, self.sizes, self.max_det)
+        if self.do_gather:
+            return unpack_gathered(self.gathered[k], self.sizes, self.max_det)
+        # no collective: this rank's own images only (its shard, in order)
+        return unpack_gathered(self.pipe.nms[k].buf, [self.batch], self.max_det)
 
     def close(self):
         torch.cuda.synchronize(self.engine.device)

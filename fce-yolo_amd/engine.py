@@ -11,7 +11,6 @@ max_nms 30000, max_wh 7680) and returns the same per-image (k, 6) tensors and ke
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
@@ -22,7 +21,10 @@ _DT = {torch.float16: N.F16, torch.float32: N.F32, torch.uint8: N.U8}
 
 
 class Engine:
-    def __init__(self, model, batch: int, imgsz: int | tuple[int, int], device=None, graph: bool = False):
+    def __init__(self, model, batch: int, imgsz: int | tuple[int, int], device=None, graph: bool = False,
+                 autotune: bool | None = None):
+        """`autotune`: time every conv's kernel variants at plan and keep the fastest (None: unless the
+        environment sets FCE_AUTOTUNE=0)."""
         if isinstance(imgsz, int):
             imgsz = (imgsz, imgsz)
         self.H, self.W = imgsz
@@ -36,7 +38,10 @@ class Engine:
         with torch.no_grad():
             x = self.be.input_view(batch, model.yaml.get("channels", 3))
             model.emit(self.be, x)
-        N.call("fce_net_plan", self.be.net, batch, self.H, self.W)
+        if autotune is None:
+            N.call("fce_net_plan", self.be.net, batch, self.H, self.W)
+        else:
+            N.call("fce_net_plan_ex", self.be.net, batch, self.H, self.W, 0 if autotune else N.PLAN_NO_AUTOTUNE)
         self.anchors = N.lib().fce_net_num_anchors(self.be.net)
         self.nc = model.model[-1].nc
         self.pred = torch.empty((batch, 4 + self.nc, self.anchors), dtype=torch.float32, device=self.device)
@@ -84,15 +89,7 @@ class Engine:
     def clone(self) -> "Engine":
         """A second executor of the same model and shapes with its own arena, pinned to this one's kernel
         variants (no second autotune): a lane of a multi-lane Pipeline."""
-        old = os.environ.get("FCE_AUTOTUNE")
-        os.environ["FCE_AUTOTUNE"] = "0"
-        try:
-            e = Engine(self.model, self.batch, (self.H, self.W), self.device, graph=self.graph)
-        finally:
-            if old is None:
-                del os.environ["FCE_AUTOTUNE"]
-            else:
-                os.environ["FCE_AUTOTUNE"] = old
+        e = Engine(self.model, self.batch, (self.H, self.W), self.device, graph=self.graph, autotune=False)
         for i in range(self.num_ops()):
             if self.variants(i):
                 e.set_variant(i, self.variant(i))
@@ -235,11 +232,12 @@ class Pipeline:
 
     With `lanes` > 1 the pipeline keeps that many batches in flight: lane l = slot % lanes owns an
     executor (``Engine.clone``: its own arena, the same kernel variants) and a stream, and runs forward
-    then NMS of its batches in order on that stream.  The lanes share the GPU, so the latency-bound
+    then NMS of its batches in order on that stream.  `x` is recorded on the lane stream
+    (``record_stream``), so the caller may drop its reference right after `submit`.  The lanes share the GPU, so the latency-bound
     40^2 / 20^2 layers and the NMS of one batch run beside the full-width early layers of the next
     (n-fce 640 bs32: 1.48 -> 1.16 ms per batch, forward only, ``scripts/dual_engine.py``).  Every batch
     still gets the bitwise result of the sequential path.  A lane reads `x` asynchronously: the caller
-    must leave `x` unchanged until that batch's `wait(slot)` / `results(slot)`.  `post` runs on one
+    must not write into `x` until that batch's `wait(slot)` / `results(slot)`.  `post` runs on one
     side stream in submission order (collectives stay ordered across ranks).
     """
 
@@ -286,6 +284,7 @@ class Pipeline:
         s.wait_event(self.in_ready[k])
         if self.used[k] and self.post is not None:
             s.wait_event(self.nms_done[k])  # the side stream's post(k) has read nms[k]
+        x.record_stream(s)  # the lane reads x asynchronously: its block stays allocated until the lane has
         with torch.cuda.stream(s):
             eng(x, out=self.preds[k], best=self.bests[k])
             self.fwd_done[k].record(s)

@@ -24,10 +24,12 @@ def _u(rng, shape, lo, hi):
     return (rng.random(shape, dtype=np.float64) * (hi - lo) + lo).astype(np.float32)
 
 
-def seeded_state_dict(keys_shapes, seed: int = 0, cls_bias=(-2.6, -1.4)):
+def seeded_state_dict(keys_shapes, seed: int = 0, cls_bias=(-2.6, -1.4), gain: float = 1.0):
     """Return {key: tensor} for an ordered iterable of (key, shape).
 
-    * 4-D weights: N(0, 1) * sqrt(1 / fan_in) (depthwise: fan_in = 9).
+    * 4-D weights: N(0, 1) * gain * sqrt(1 / fan_in) (depthwise: fan_in = 9).  gain 1 (the default, every
+      committed fixture and the bench) lets the signal decay with depth; gain ~1.6 keeps the outputs
+      input-dependent (the margin-designed end-to-end NMS fixture, make_golden_e2e_nms.py).
     * BN: weight U(0.6,1.4), bias U(-0.3,0.3), running_mean U(-0.3,0.3), running_var U(0.5,1.5).
     * conv biases U(-0.2, 0.2); the final Detect cls conv bias U(cls_bias) so that only a
       fraction of anchors passes conf=0.25; BiFPN ``w`` U(0.3, 1.5).
@@ -51,7 +53,7 @@ def seeded_state_dict(keys_shapes, seed: int = 0, cls_bias=(-2.6, -1.4)):
             a = _u(rng, shape, 0.5, 1.5)
         elif len(shape) == 4:
             fan_in = shape[1] * shape[2] * shape[3]
-            a = (rng.standard_normal(shape) * math.sqrt(1.0 / fan_in)).astype(np.float32)
+            a = (rng.standard_normal(shape) * (gain * math.sqrt(1.0 / fan_in))).astype(np.float32)
         elif _is(key, "w") and len(shape) == 1:
             a = _u(rng, shape, 0.3, 1.5)
         elif _is(key, "bias"):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 4
+#define FCE_ABI_VERSION 5
 
 /* status codes */
 #define FCE_OK 0
@@ -261,8 +261,13 @@ int fce_net_add_detect(fce_net* net, int nl, const int* map_bufs, const float* s
  * the anchor blocks (offsets are resolved at plan time). */
 int fce_net_add_conv_detect(fce_net* net, const fce_conv_desc* d, int in_buf, int in_coff, int part, int level,
                             float stride, int nc, int reg_max, const void* w_packed, const float* bias);
-/* allocate the arena for (batch, H, W); invalidates any captured graph */
+/* allocate the arena for (batch, H, W); invalidates any captured graph.  Times every candidate kernel
+ * variant of every conv and keeps the fastest unless the environment sets FCE_AUTOTUNE=0. */
 int fce_net_plan(fce_net* net, int batch, int h, int w);
+/* fce_net_plan with explicit options instead of the environment (ABI v5):
+ * FCE_PLAN_NO_AUTOTUNE keeps the heuristic variants (e.g. a second executor that copies another's picks). */
+#define FCE_PLAN_NO_AUTOTUNE 1
+int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags);
 size_t fce_net_arena_bytes(const fce_net* net);
 int fce_net_num_anchors(const fce_net* net);
 /* input: NCHW f16/f32/u8 (u8 is divided by 255 in the stem); pred: (batch, 4+nc, A) fp32.

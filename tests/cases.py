@@ -191,3 +191,34 @@ def compare_full(y, fx, anchors=True):
     n = y.shape[2] if anchors else y.shape[2] * y.shape[3]
     e_sum = ((sums - torch.from_numpy(fx["sum"])).abs().max() / (scale * n)).item()
     return e_slice, e_sum
+
+
+# ---------------------------------------------------------------- margin-designed end-to-end NMS (golden/e2e_nms.npz)
+E2E_NMS = {
+    # fixture key: (cfg, batch, imgsz) -- make_golden_e2e_nms.CASES
+    "yolo11n-fce_320_b2": ("yolo11n-fce.yaml", 2, 320),
+    "yolo11s-bifpn_160_b2": ("yolo11s-bifpn.yaml", 2, 160),
+}
+
+
+def designed_model(key, fx):
+    """(model, input) of a margin-designed end-to-end NMS case: seeded_state_dict(keys, 0, gain) with the
+    Detect cls head's last 1x1 convs replaced by the fixture's designed weights (make_golden_e2e_nms.py)."""
+    import re
+
+    from fce_yolo_amd.parser import DetectionModel, load_cfg
+
+    cfg, b, s = E2E_NMS[key]
+    model = DetectionModel(load_cfg(cfg))
+    sd = seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0, gain=float(fx["gain"]))
+    det = len(model.model) - 1
+    n = 0
+    for k in sd:
+        m = re.match(rf"^model\.{det}\.cv3\.(\d+)\.2\.(weight|bias)$", k)
+        if m:
+            sd[k] = torch.from_numpy(fx[f"cls_{m.group(2)[0]}{m.group(1)}"].copy())
+            n += 1
+    assert n == 6, n
+    model.load_state_dict(sd)
+    x = torch.rand(b, 3, s, s, generator=torch.Generator().manual_seed(int(fx["x_seed"])))
+    return model.eval(), x

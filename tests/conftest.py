@@ -53,6 +53,11 @@ def full_fx():
 
 
 @pytest.fixture(scope="session")
+def e2e_nms_fx():
+    return _Npz(GOLDEN / "e2e_nms.npz")
+
+
+@pytest.fixture(scope="session")
 def nms_fx():
     return _Npz(GOLDEN / "nms.npz")
 

@@ -129,3 +129,32 @@ def test_sharded_gather_restores_unsharded_order_gloo_world2(total, bs):
     for _, keep, first in res:
         assert keep == want
         assert first == [float(g) for g in range(total)]
+
+
+def _empty_shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fce_yolo_amd.dist import ShardedPredictor
+
+        try:  # 1 image over 2 ranks: rank 1's shard is empty; BOTH ranks must refuse (no one reaches a collective)
+            ShardedPredictor(None, 1, 320, "cpu", batch_size=1)
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, "ValueError" if "empty shard" in str(e) else str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_predictor_empty_shard_raises_on_every_rank_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, "ValueError"), (1, "ValueError")]

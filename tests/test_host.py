@@ -92,7 +92,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(L, s)]
     assert not missing, missing
     assert declared <= set(N.EXPORTED) | {"fce_net_create", "fce_net_destroy"}
-    assert L.fce_abi_version() == 4
+    assert L.fce_abi_version() == 5
 
 
 def test_device_count_without_gpu_is_safe():
@@ -205,3 +205,50 @@ def test_library_has_no_undefined_internal_symbols():
     out = subprocess.run(["nm", "-uC", str(N.LIB_PATH)], capture_output=True, text=True, check=True).stdout
     bad = [l for l in out.splitlines() if "fce::" in l]
     assert not bad, bad
+
+
+def _bench_env(**kw):
+    import os
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def test_bench_gpus_n_launches_ranks_before_torch():
+    """`python bench.py --gpus 2` (no WORLD_SIZE) starts torch.distributed.run with 2 ranks on 127.0.0.1 as a
+    child process, decided before torch (let alone the GPU) is touched in the launcher."""
+    import json
+    import subprocess
+    import sys
+
+    root = Path(__file__).resolve().parents[1]
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "3"], capture_output=True,
+                       text=True, timeout=120, env=_bench_env(FCE_BENCH_DRY_LAUNCH="1"))
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["torch_imported"] is False
+    cmd = d["launch"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    # a rank (WORLD_SIZE set) or one GPU: no launcher
+    sys.path.insert(0, str(root))
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", root / "bench.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.launch_command(["--gpus", "8"], {"WORLD_SIZE": "8"}) is None
+    assert m.launch_command(["--gpus", "1"], {}) is None
+    assert m.launch_command([], {}) is None
+
+
+def test_bench_world_size_mismatch_fails():
+    import subprocess
+    import sys
+
+    root = Path(__file__).resolve().parents[1]
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "4"], capture_output=True, text=True,
+                       timeout=300, env=_bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE 2" in r.stderr, (r.returncode, r.stderr[-500:])

@@ -93,6 +93,20 @@ def test_oracle_nms_on_model_output(e2e_fx):
         assert np.array_equal(dets[b], fx[f"nms_det{b}"])
 
 
+@pytest.mark.parametrize("key", list(cases.E2E_NMS))
+def test_oracle_designed_end_to_end_nms_matches_reference(key, e2e_nms_fx):
+    """Margin-designed end-to-end case (make_golden_e2e_nms.py): the oracle's fp32 forward + oracle NMS keep
+    exactly the anchors the reference's forward + non_max_suppression kept, with the same rows to 1e-4."""
+    fx = e2e_nms_fx.group(key)
+    model, x = cases.designed_model(key, fx)
+    y = cases.oracle_model(model, x, torch.float32).numpy()
+    assert np.abs(y[:, :, ::7] - fx["y_slice"]).max() <= 1e-4 * np.abs(fx["y_slice"]).max()
+    dets, keeps = nms_oracle.non_max_suppression(y)
+    for b in range(x.shape[0]):
+        assert np.array_equal(keeps[b], fx[f"keep{b}"]), b
+        assert np.abs(dets[b] - fx[f"det{b}"]).max() <= 1e-4 * max(1.0, np.abs(fx[f"det{b}"]).max()), b
+
+
 def _cfg(name):
     """The built-in graph data of the product package (restated from the reference YAMLs)."""
     from fce_yolo_amd.parser import load_cfg
