@@ -10,7 +10,8 @@ preprocess / pre_transform, models/yolo/detect/predict.py:33-121 postprocess + c
 
 Letterbox placement is computed on the host exactly as LetterBox.__call__ does (augment.py:1575-1605,
 Python round); images of any size share one (H, W) canvas (auto=False, the predictor's setting for
-batched inputs of mixed shapes).
+batched inputs of mixed shapes).  `Predictor` keeps several batches in flight (pinned staging, one H2D and
+one D2H copy per batch, an executor lane with a captured hipGraph per slot).
 """
 
 from __future__ import annotations
@@ -78,49 +79,169 @@ class Letterbox:
         return self.out[: len(imgs)]
 
 
+class _Slot:
+    """One batch in flight: pinned host staging (descriptors + packed source images), the device copy of it,
+    the u8 canvas, an executor lane (own arena, own stream, captured hipGraph), NMS, pinned results."""
+
+    def __init__(self, eng: Engine, batch: int, device, nms_kw):
+        self.eng = eng
+        self.stream = torch.cuda.Stream(device)
+        self.canvas = torch.empty((batch, 3, eng.H, eng.W), dtype=torch.uint8, device=device)
+        self.pred = torch.empty_like(eng.pred)
+        self.best = eng.new_best()
+        self.nms = NMS(batch, eng.anchors, eng.nc, device, **nms_kw)
+        self.out_host = torch.empty(self.nms.buf.numel(), dtype=torch.uint8, pin_memory=True)
+        self.done = torch.cuda.Event()
+        self.host = self.dev = None
+        self.ticket = None  # ticket whose results this slot holds (not yet collected)
+        self.shapes = []
+
+    def reserve(self, nbytes: int, device):
+        if self.host is None or self.host.numel() < nbytes:
+            cap = max(nbytes, 1 << 20)
+            cap += cap // 4  # headroom: a slightly larger batch of images does not re-pin
+            self.host = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self.dev = torch.empty(cap, dtype=torch.uint8, device=device)
+
+
 class Predictor:
     """predict(images) -> per image (k, 6) [x1, y1, x2, y2, conf, cls] in source pixels (+ anchor indices).
 
-    Fixed batch capacity; a call with fewer images pads the batch with the last canvas (their results are
-    dropped).  All stages run on the device stream of the caller; one host sync at the end (counts)."""
+    The reference's predict loop (engine/predictor.py:151-182 preprocess, :276-381 stream_inference) as a
+    pipeline of `lanes` batches in flight on the device.  `submit(images)` returns a ticket at once:
 
-    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300):
-        self.engine = Engine(model, batch, imgsz, device)
+      * the decoded uint8 HWC images are packed by a host thread pool into this slot's PINNED staging buffer
+        behind the letterbox / box-scale descriptors (built on the host exactly as LetterBox.__call__ and
+        ops.scale_boxes compute them), and go to the device in ONE async H2D copy on the slot's stream;
+      * device letterbox -> forward (the slot's executor lane replays its captured hipGraph) -> NMS with the
+        Detect epilogue's best-class keys -> scale_boxes, all on that stream;
+      * the packed NMS outputs come back in one async D2H copy into pinned memory.
+
+    `result(ticket)` waits for that batch only and returns host tensors.  Slots are reused round-robin; a
+    slot's results not collected by then are kept on the host.  A call with fewer images than `batch`
+    repeats the last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
+
+    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 3,
+                 graph: bool = True, workers: int | None = None):
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.engine = Engine(model, batch, imgsz, device, graph=graph)
         self.device = self.engine.device
         self.batch = batch
-        self.lb = Letterbox(batch, (self.engine.H, self.engine.W), self.device)
-        self.nms = NMS(batch, self.engine.anchors, self.engine.nc, self.device, conf, iou, max_det)
-        self.scales = torch.empty(batch * C.sizeof(BoxScale), dtype=torch.uint8, device=self.device)
+        self.max_det = max_det
+        nms_kw = dict(conf=conf, iou=iou, max_det=max_det)
+        engs = [self.engine] + [self.engine.clone() for _ in range(max(1, lanes) - 1)]
+        for e in engs:
+            e.graph = graph
+        self.slots = [_Slot(e, batch, self.device, nms_kw) for e in engs]
+        self.nms = self.slots[0].nms  # slot 0's NMS (API compatibility)
+        self.lb = Letterbox(batch, (self.engine.H, self.engine.W), self.device)  # standalone use
+        self.pool = ThreadPoolExecutor(workers or max(1, min(8, (os.cpu_count() or 2) // 2)))
+        self._next = 0
+        self._ready = {}  # ticket -> results collected early (slot reused before result())
+        self._tickets = 0
+
+    def _desc_bytes(self) -> int:
+        return (self.batch * (C.sizeof(LetterboxImg) + C.sizeof(BoxScale)) + 255) // 256 * 256
+
+    def submit(self, images) -> int:
+        if not 0 < len(images) <= self.batch:
+            raise ValueError(f"Predictor: 1..{self.batch} images per call")
+        imgs = [np.ascontiguousarray(im) for im in images]
+        for im in imgs:
+            if im.dtype != np.uint8 or im.ndim != 3 or im.shape[2] != 3:
+                raise ValueError("Predictor: images must be uint8 (h, w, 3) BGR arrays")
+        k = self._next
+        self._next = (k + 1) % len(self.slots)
+        sl = self.slots[k]
+        if sl.ticket is not None:  # the slot's previous batch: collect it before its buffers are reused
+            self._ready[sl.ticket] = self._collect(sl)
+        n = len(imgs)
+        H, W = self.engine.H, self.engine.W
+        db = self._desc_bytes()
+        offs, off = [], db
+        for im in imgs:
+            offs.append(off)
+            off += (im.nbytes + 255) // 256 * 256
+        sl.reserve(off, self.device)
+        sl.done.synchronize()  # (already collected above) the staging buffers are free
+        hbase, dbase = sl.host.data_ptr(), sl.dev.data_ptr()
+        hnp = sl.host.numpy()
+        futs = [self.pool.submit(np.copyto, hnp[o:o + im.nbytes].reshape(im.shape), im) for o, im in zip(offs, imgs)]
+        lbd = (LetterboxImg * n)()
+        scd = (BoxScale * self.batch)()
+        for i, im in enumerate(imgs):
+            h0, w0 = int(im.shape[0]), int(im.shape[1])
+            new_h, new_w, top, left = letterbox_geometry(h0, w0, H, W)
+            lbd[i] = LetterboxImg(dbase + offs[i], h0, w0, w0 * 3, new_h, new_w, top, left)
+        for i in range(self.batch):
+            h0, w0 = imgs[min(i, n - 1)].shape[:2]
+            gain, px, py = box_scale(H, W, int(h0), int(w0))
+            scd[i] = BoxScale(gain, px, py, int(h0), int(w0))
+        nlb = self.batch * C.sizeof(LetterboxImg)
+        C.memmove(hbase, lbd, C.sizeof(lbd))
+        C.memmove(hbase + nlb, scd, C.sizeof(scd))
+        for f in futs:
+            f.result()
+        main = torch.cuda.current_stream(self.device)
+        sl.stream.wait_stream(main)
+        with torch.cuda.stream(sl.stream):
+            sl.dev[:off].copy_(sl.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
+            st = sl.stream.cuda_stream
+            N.call("fce_letterbox", C.c_void_p(dbase), n, C.c_void_p(sl.canvas.data_ptr()), H, W, self.lb.pad, st)
+            if n < self.batch:  # fixed-shape engine: pad the batch by repeating the last canvas
+                sl.canvas[n:].copy_(sl.canvas[n - 1:n].expand(self.batch - n, -1, -1, -1))
+            sl.eng(sl.canvas, out=sl.pred, best=sl.best)
+            dets, keep, counts = sl.nms(sl.pred, sl.best)
+            N.call("fce_scale_boxes", C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()), self.batch,
+                   self.max_det, C.c_void_p(dbase + nlb), st)
+            sl.out_host.copy_(sl.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
+            sl.done.record(sl.stream)
+        self._tickets += 1
+        sl.ticket = self._tickets
+        sl.shapes = [im.shape[:2] for im in imgs]
+        return sl.ticket
+
+    def _collect(self, sl: _Slot):
+        sl.done.synchronize()
+        keep, dets, counts = NMS.unpack(sl.out_host, self.batch, self.max_det)
+        n = len(sl.shapes)
+        cnt = counts[:n].tolist()
+        res = ([dets[i, :cnt[i]].clone() for i in range(n)], [keep[i, :cnt[i]].clone() for i in range(n)])
+        sl.ticket = None
+        return res
+
+    def result(self, ticket: int, return_idxs: bool = False):
+        """Per image (k, 6) host tensors of a submitted batch (+ kept anchor indices)."""
+        if ticket in self._ready:
+            d, k = self._ready.pop(ticket)
+        else:
+            sl = next((s for s in self.slots if s.ticket == ticket), None)
+            if sl is None:
+                raise KeyError(f"Predictor: unknown or already collected ticket {ticket}")
+            d, k = self._collect(sl)
+        return (d, k) if return_idxs else d
 
     def __call__(self, images, return_idxs: bool = False):
         if len(images) == 0:
             return ([], []) if return_idxs else []
-        if len(images) > self.batch:
-            raise ValueError(f"Predictor: at most {self.batch} images per call")
-        imgs = [torch.as_tensor(np.ascontiguousarray(im)) if isinstance(im, np.ndarray) else im for im in images]
-        imgs = [im.to(self.device, non_blocking=True) for im in imgs]
-        canvas = self.lb(imgs)
-        n = len(imgs)
-        if n < self.batch:  # fixed-shape engine: pad the batch by repeating the last canvas
-            full = self.lb.out
-            full[n:].copy_(full[n - 1:n].expand(self.batch - n, -1, -1, -1))
-            canvas = full
-        pred = self.engine(canvas)
-        dets, keep, counts = self.nms(pred)
-        H, W = self.engine.H, self.engine.W
-        host = (BoxScale * self.batch)()
-        for i in range(self.batch):
-            im = imgs[min(i, n - 1)]
-            h0, w0 = int(im.shape[0]), int(im.shape[1])
-            gain, px, py = box_scale(H, W, h0, w0)
-            host[i] = BoxScale(gain, px, py, h0, w0)
-        self.scales[: C.sizeof(host)].copy_(torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8))
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        N.call("fce_scale_boxes", C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()), self.batch,
-               self.nms.max_det, C.c_void_p(self.scales.data_ptr()), stream)
-        d, k = self.nms.results()
-        d, k = d[:n], k[:n]
-        return (d, k) if return_idxs else d
+        return self.result(self.submit(images), return_idxs)
+
+    def stream(self, batches, return_idxs: bool = False):
+        """Generator over an iterable of image batches with `lanes` batches in flight (results in order)."""
+        from collections import deque
+
+        q = deque()
+        for imgs in batches:
+            if len(q) == len(self.slots):
+                yield self.result(q.popleft(), return_idxs)
+            q.append(self.submit(imgs))
+        while q:
+            yield self.result(q.popleft(), return_idxs)
 
     def close(self):
-        self.engine.close()
+        torch.cuda.synchronize(self.device)
+        self.pool.shutdown()
+        for s in self.slots:
+            s.eng.close()

@@ -196,8 +196,8 @@ def compare_full(y, fx, anchors=True):
 # ---------------------------------------------------------------- margin-designed end-to-end NMS (golden/e2e_nms.npz)
 E2E_NMS = {
     # fixture key: (cfg, batch, imgsz) -- make_golden_e2e_nms.CASES
-    "yolo11n-fce_320_b2": ("yolo11n-fce.yaml", 2, 320),
-    "yolo11s-bifpn_160_b2": ("yolo11s-bifpn.yaml", 2, 160),
+    "yolo11n-fce_256_b2": ("yolo11n-fce.yaml", 2, 256),
+    "yolo11s-bifpn_256_b2": ("yolo11s-bifpn.yaml", 2, 256),
 }
 
 

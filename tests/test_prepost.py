@@ -139,3 +139,31 @@ def test_predictor_end_to_end_vs_oracle(device):
         got = dets[i].cpu().numpy()
         assert np.array_equal(got[:, :4], ref) and np.array_equal(got[:, 4:], od[i][:, 4:])
     pred.close()
+
+
+@pytest.mark.gpu
+def test_predictor_stream_matches_one_at_a_time(device):
+    """The overlapped predictor (3 slots in flight: pinned staging, one H2D / D2H copy per batch, hipGraph
+    lanes) gives every batch exactly what a one-lane, direct-launch predictor gives it; partial batches,
+    more batches than slots, and results collected out of order after their slots were reused."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    rng = np.random.default_rng(4)
+    batches = [_images(rng, [(240, 320), (320, 200), (150, 150), (480, 640)]), _images(rng, [(100, 333)]),
+               _images(rng, [(320, 320)] * 4), _images(rng, [(64, 512), (512, 64), (300, 301)]),
+               _images(rng, [(200, 180)] * 4)]
+    p1 = P.Predictor(model, 4, 320, device, lanes=1, graph=False)
+    seq = [p1(b, return_idxs=True) for b in batches]
+    p1.close()
+    p3 = P.Predictor(model, 4, 320, device, lanes=3)
+
+    def same(a, b):
+        return len(a[0]) == len(b[0]) and all(torch.equal(x, y) for x, y in zip(a[0] + a[1], b[0] + b[1]))
+
+    for i, r in enumerate(p3.stream(batches, return_idxs=True)):
+        assert same(r, seq[i]), i
+    tickets = [p3.submit(b) for b in batches]  # 5 batches over 3 slots: two collected early
+    for i in reversed(range(len(batches))):
+        assert same(p3.result(tickets[i], return_idxs=True), seq[i]), i
+    with pytest.raises(KeyError):
+        p3.result(tickets[0])
+    p3.close()
