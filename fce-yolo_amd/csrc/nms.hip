@@ -73,11 +73,14 @@ static int next_pow2(int v) {
   return p;
 }
 
+static size_t nms2_ws_per_image(int A, int max_nms);
+
 static size_t nms_ws_per_image(int A, int C, int max_nms) {
   const size_t M = std::min(C, max_nms);
   const size_t P2 = next_pow2(std::max(C, 1));
   auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-  return al(size_t(A) * 4) * 2 + al(size_t(C) * 4) * 4 + size_t(C) * 16 + P2 * 8 + al(M * 4);
+  const size_t v1 = al(size_t(A) * 4) * 2 + al(size_t(C) * 4) * 4 + size_t(C) * 16 + P2 * 8 + al(M * 4);
+  return (std::max(v1, nms2_ws_per_image(A, max_nms)) + 255) & ~size_t(255);  // either path fits (chosen per call)
 }
 
 static int nms_cap(int A, int nc, int multi) { return multi && nc > 1 ? A * nc : A; }
@@ -681,6 +684,401 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
   if (threadIdx.x == 0) counts[n] = s_kept;
 }
 
+
+// ================================================================ multi-workgroup NMS (the default path)
+// The one-workgroup kernel above needs a whole CU per image (1024 threads, 112 KB of LDS), so beside the
+// forward of other batches it waits for CUs to drain, and its candidate and sort phases are serial over
+// one workgroup.  Here the same computation is four launches:
+//   K1 nms2_keys_kernel   (all CUs, one thread per anchor): best class (the Detect epilogue's key, or the
+//                          arg-max over the class rows) and the sort key score bits << 32 | ~anchor (0 for
+//                          a non-candidate).  Descending keys = (score desc, anchor asc) = the reference's
+//                          order of candidates (they are formed in anchor order, nms.py:101-105, 150-153);
+//   K2 nms2_sort_kernel   (one 256-thread workgroup per 2048-anchor chunk): bitonic sort of the chunk's
+//                          keys in 16 KB of LDS, candidate count per chunk;
+//   K3 nms2_rank_kernel   (one workgroup per chunk): a candidate's global rank = its rank in its chunk +
+//                          the number of larger keys in every other chunk (binary searches); ranks <
+//                          max_nms scatter the class-offset box, area, anchor, score and class into
+//                          rank-ordered arrays (the truncation of nms.py:155-156), and flag degenerate boxes;
+//   K4 nms2_greedy_kernel (one 256-thread workgroup per image, LDS = max_nms bytes + max_det kept boxes):
+//                          the tiled greedy of the kernel above over the rank-ordered arrays (coalesced),
+//                          or the literal loop when a box is degenerate.
+// Same fp32 arithmetic, same order, same greedy: bitwise the results of nms_kernel.
+static constexpr int NMS2_CH = 2048;
+static constexpr int NMS2_SORT_THREADS = 256;
+static constexpr int NMS2_G_THREADS = 256;
+static constexpr int NMS2_G_WAVES = NMS2_G_THREADS / 64;
+
+struct Nms2Ws {
+  uint64_t* keys;  // [A2] per anchor, then sorted within each chunk (descending)
+  int* acls;       // [A] best class per anchor
+  int* ccount;     // [NCH] candidates per chunk
+  int* flags;      // [4]: [0] = a degenerate box among the first M sorted candidates
+  float4* sbox;    // [Mc] rank-ordered class-offset xyxy boxes
+  float* sarea;    // [Mc]
+  int* sanc;       // [Mc] anchor
+  float* sscore;   // [Mc]
+  int* scls;       // [Mc]
+};
+
+__host__ __device__ inline int nms2_a2(int A) { return (A + NMS2_CH - 1) / NMS2_CH * NMS2_CH; }
+
+static size_t nms2_ws_per_image(int A, int max_nms) {
+  auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t A2 = nms2_a2(A), NCH = A2 / NMS2_CH, Mc = std::min(A, max_nms);
+  return A2 * 8 + al(size_t(A) * 4) + al(NCH * 4) + 16 + Mc * 16 + 4 * al(Mc * 4);
+}
+
+__device__ Nms2Ws carve2(char* p, int A, int Mc) {
+  auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t A2 = nms2_a2(A), NCH = A2 / NMS2_CH;
+  Nms2Ws w;
+  w.keys = reinterpret_cast<uint64_t*>(p);
+  p += A2 * 8;
+  w.acls = reinterpret_cast<int*>(p);
+  p += al(size_t(A) * 4);
+  w.ccount = reinterpret_cast<int*>(p);
+  p += al(NCH * 4);
+  w.flags = reinterpret_cast<int*>(p);
+  p += 16;
+  w.sbox = reinterpret_cast<float4*>(p);
+  p += size_t(Mc) * 16;
+  w.sarea = reinterpret_cast<float*>(p);
+  p += al(size_t(Mc) * 4);
+  w.sanc = reinterpret_cast<int*>(p);
+  p += al(size_t(Mc) * 4);
+  w.sscore = reinterpret_cast<float*>(p);
+  p += al(size_t(Mc) * 4);
+  w.scls = reinterpret_cast<int*>(p);
+  return w;
+}
+
+__global__ __launch_bounds__(256) void nms2_keys_kernel(const float* pred, const unsigned long long* bestk, int nc, int A,
+                                                        int Mc, float conf_thres, char* ws, size_t per,
+                                                        NmsClassMask cm) {
+  const int n = blockIdx.y;
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  Nms2Ws w = carve2(ws + size_t(n) * per, A, Mc);
+  uint64_t key = 0;
+  if (a < A) {
+    float best = -INFINITY;
+    int bj = 0;
+    if (bestk) {  // fused into the Detect cls epilogue: score bits << 32 | ~class
+      const unsigned long long k = bestk[int64_t(n) * A + a];
+      best = __uint_as_float(uint32_t(k >> 32));
+      bj = int(0xFFFFFFFFu - uint32_t(k));
+    } else {  // first maximum over the class rows (torch.max, nms.py:101)
+      const float* p = pred + (int64_t(n) * (4 + nc) + 4) * A + a;
+      int c = 0;
+      for (; c + 8 <= nc; c += 8) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = p[int64_t(c + j) * A];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best) {
+            best = v[j];
+            bj = c + j;
+          }
+      }
+      for (; c < nc; ++c) {
+        const float v = p[int64_t(c) * A];
+        if (v > best) {
+          best = v;
+          bj = c;
+        }
+      }
+    }
+    const bool allowed = !cm.on || (bj < 1024 && ((cm.w[bj >> 5] >> (bj & 31)) & 1u));
+    if (best > conf_thres && allowed)  // a positive score: its bits order like the value
+      key = (uint64_t(__float_as_uint(best)) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(a));
+    w.acls[a] = bj;
+  }
+  if (a < nms2_a2(A)) w.keys[a] = key;
+}
+
+__global__ __launch_bounds__(NMS2_SORT_THREADS) void nms2_sort_kernel(int A, int Mc, char* ws, size_t per) {
+  __shared__ uint64_t sk[NMS2_CH];
+  __shared__ int scount;
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  Nms2Ws w = carve2(ws + size_t(n) * per, A, Mc);
+  uint64_t* g = w.keys + size_t(chunk) * NMS2_CH;
+  if (threadIdx.x == 0) scount = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int i = threadIdx.x; i < NMS2_CH; i += NMS2_SORT_THREADS) {
+    const uint64_t k = g[i];
+    sk[i] = k;
+    cnt += k != 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&scount, cnt);
+  __syncthreads();
+  if (scount > 0) bitonic_desc(sk, NMS2_CH);  // ends with __syncthreads
+  for (int i = threadIdx.x; i < NMS2_CH; i += NMS2_SORT_THREADS) g[i] = sk[i];
+  if (threadIdx.x == 0) {
+    w.ccount[chunk] = scount;
+    if (chunk == 0) w.flags[0] = 0;
+  }
+}
+
+// number of keys > k in a descending run of `cnt` distinct keys
+__device__ __forceinline__ int count_greater(const uint64_t* run, int cnt, uint64_t k) {
+  int lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (run[mid] > k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void nms2_rank_kernel(const float* pred, int nc, int A, int Mc, int max_nms,
+                                                        float max_wh, char* ws, size_t per) {
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  Nms2Ws w = carve2(ws + size_t(n) * per, A, Mc);
+  const int nch = nms2_a2(A) / NMS2_CH;
+  int total = 0;
+  for (int r = 0; r < nch; ++r) total += w.ccount[r];
+  const int M = min(total, max_nms);
+  const int mine = w.ccount[chunk];
+  const uint64_t* run = w.keys + size_t(chunk) * NMS2_CH;
+  const float* P = pred + int64_t(n) * (4 + nc) * A;
+  int deg = 0;
+  for (int i = threadIdx.x; i < mine; i += 256) {
+    const uint64_t k = run[i];
+    int rank = i;
+    for (int r = 0; r < nch; ++r)
+      if (r != chunk) rank += count_greater(w.keys + size_t(r) * NMS2_CH, w.ccount[r], k);
+    if (rank >= M) continue;
+    const int a = int(0xFFFFFFFFu - uint32_t(k));
+    const int j = w.acls[a];
+    const float cx = P[a], cy = P[int64_t(1) * A + a];
+    const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
+    const float off = (float)j * max_wh;
+    const float bx1 = (cx - hw) + off, by1 = (cy - hh) + off, bx2 = (cx + hw) + off, by2 = (cy + hh) + off;
+    const float ar = (bx2 - bx1) * (by2 - by1);
+    w.sbox[rank] = make_float4(bx1, by1, bx2, by2);
+    w.sarea[rank] = ar;
+    w.sanc[rank] = a;
+    w.sscore[rank] = __uint_as_float(uint32_t(k >> 32));
+    w.scls[rank] = j;
+    deg |= !(ar > 0.0f) || !isfinite(ar);
+  }
+  if (__any(deg) && (threadIdx.x & 63) == 0) atomicOr(w.flags, 1);
+}
+
+__global__ __launch_bounds__(NMS2_G_THREADS) void nms2_greedy_kernel(const float* pred, int nc, int A, int Mc,
+                                                                     float iou_thres, int max_det, int max_nms,
+                                                                     char* ws, size_t per, float* dets,
+                                                                     int64_t* keep, int32_t* counts) {
+  extern __shared__ __attribute__((aligned(16))) char g2pool[];  // removed [Mc] | kbox | karea | kidx
+  __shared__ int tile_idx[TILE];
+  __shared__ float4 tile_box[TILE];
+  __shared__ float tile_area[TILE];
+  __shared__ uint64_t colmask[TILE];
+  __shared__ int s_tile_n, s_need, s_next, s_nk, s_done, s_kept;
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Nms2Ws w = carve2(ws + size_t(n) * per, A, Mc);
+  const int nch = nms2_a2(A) / NMS2_CH;
+  int total = 0;
+  for (int r = 0; r < nch; ++r) total += w.ccount[r];
+  const int M = min(total, max_nms);
+  const bool degenerate = w.flags[0] != 0;
+  const float* P = pred + int64_t(n) * (4 + nc) * A;
+  uint8_t* lremoved = reinterpret_cast<uint8_t*>(g2pool);
+  float4* kbox = reinterpret_cast<float4*>(g2pool + ((Mc + 15) & ~15));
+  float* karea = reinterpret_cast<float*>(kbox + max_det);
+  int* kidx = reinterpret_cast<int*>(karea + max_det);
+  auto emit_det = [&](int pos, int slot) {
+    const int a = w.sanc[pos];
+    const float cx = P[a], cy = P[int64_t(1) * A + a];
+    const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
+    float* d = dets + (int64_t(n) * max_det + slot) * 6;
+    d[0] = cx - hw;
+    d[1] = cy - hh;
+    d[2] = cx + hw;
+    d[3] = cy + hh;
+    d[4] = w.sscore[pos];
+    d[5] = (float)w.scls[pos];
+    keep[int64_t(n) * max_det + slot] = a;
+  };
+  if (threadIdx.x == 0) s_kept = 0;
+  __syncthreads();
+
+  if (degenerate) {
+    // literal per-box greedy (TorchNMS.nms with its early exit, nms.py:276-296)
+    for (int i = threadIdx.x; i < M; i += NMS2_G_THREADS) lremoved[i] = 0;
+    __syncthreads();
+    int kept = 0;
+    for (int i = 0; i < M && kept < max_det; ++i) {
+      if (lremoved[i]) continue;
+      if (threadIdx.x == 0) emit_det(i, kept);
+      ++kept;
+      if (kept >= max_det) break;
+      const float4 bi = w.sbox[i];
+      const float ai = w.sarea[i];
+      int any = 0;
+      for (int j = i + 1 + threadIdx.x; j < M; j += NMS2_G_THREADS) {
+        if (lremoved[j]) continue;
+        float inter;
+        iou_ref(bi, ai, w.sbox[j], w.sarea[j], &inter);
+        any |= inter != 0.0f;
+      }
+      any = __syncthreads_or(any);
+      if (any) {
+        for (int j = i + 1 + threadIdx.x; j < M; j += NMS2_G_THREADS) {
+          if (lremoved[j]) continue;
+          float inter;
+          const float iou = iou_ref(bi, ai, w.sbox[j], w.sarea[j], &inter);
+          if (!(iou <= iou_thres)) lremoved[j] = 1;
+        }
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[n] = kept;
+    return;
+  }
+
+  // candidates [jlo, jhi) (not yet removed) against kept boxes [klo, khi): thread = (candidate, split of the
+  // kept list); every lane of a wave reads the same kept boxes (LDS broadcast)
+  auto test_range = [&](int jlo, int jhi, int klo, int khi) {
+    const int nj = jhi - jlo, nk = khi - klo;
+    if (nj <= 0 || nk <= 0) return;
+    const int rj = (nj + 63) & ~63;
+    const int S = max(1, min(nk, NMS2_G_THREADS / rj));
+    for (int idx = threadIdx.x; idx < rj * S; idx += NMS2_G_THREADS) {
+      const int j = jlo + idx % rj, sp0 = idx / rj;
+      if (j >= jhi || lremoved[j]) continue;
+      const float4 bj = w.sbox[j];
+      const float aj = w.sarea[j];
+      bool rem = false;
+      int k = klo + sp0;
+      for (; k + 3 * S < khi && !rem; k += 4 * S) {
+        float4 kb[4];
+        float ka[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          kb[u] = kbox[k + u * S];
+          ka[u] = karea[k + u * S];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rem |= suppresses(kb[u], ka[u], bj, aj, iou_thres);
+      }
+      for (; k < khi && !rem; k += S) rem = suppresses(kbox[k], karea[k], bj, aj, iou_thres);
+      if (rem) lremoved[j] = 1;
+    }
+  };
+
+  // tiled greedy with a lazy frontier (nms_kernel 3a): exact when every area > 0
+  int cursor = 0, F = 0;
+  while (true) {
+    while (true) {
+      if (wv == 0) {
+        int cnt = 0;
+        for (int c = cursor; cnt < TILE && c < F; c += 64) {
+          const int j = c + lane;
+          const bool alive = j < F && !lremoved[j];
+          const uint64_t bb = __ballot(alive);
+          const int take = min(__popcll(bb), TILE - cnt);
+          const int rank = __popcll(bb & ((1ull << lane) - 1ull));
+          if (alive && rank < take) tile_idx[cnt + rank] = j;
+          cnt += take;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const bool need = cnt < TILE && F < M;
+        if (!need && lane < cnt) {
+          const int j = tile_idx[lane];
+          tile_box[lane] = w.sbox[j];
+          tile_area[lane] = w.sarea[j];
+        }
+        if (lane == 0) {
+          s_tile_n = cnt;
+          s_need = need;
+          s_next = cnt == TILE ? tile_idx[TILE - 1] + 1 : M;
+        }
+      }
+      __syncthreads();
+      if (!s_need) break;
+      const int Fn = min(M, F + WIN);
+      for (int j = F + threadIdx.x; j < Fn; j += NMS2_G_THREADS) lremoved[j] = 0;
+      __syncthreads();
+      test_range(F, Fn, 0, s_kept);
+      F = Fn;
+      __syncthreads();
+    }
+    const int cnt = s_tile_n;
+    if (cnt == 0) break;
+    for (int u = wv; u < TILE; u += NMS2_G_WAVES) {
+      bool sup = false;
+      if (lane < u && u < cnt) sup = suppresses(tile_box[lane], tile_area[lane], tile_box[u], tile_area[u], iou_thres);
+      const uint64_t bb = __ballot(sup);
+      if (lane == 0) colmask[u] = bb;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const int kept0 = s_kept;
+      const uint64_t Cm = lane < cnt ? colmask[lane] : 0ull;
+      uint64_t undecided = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull), kept = 0;
+      while (undecided) {
+        const bool me = (undecided >> lane) & 1ull;
+        const uint64_t k = __ballot(me && (Cm & (kept | undecided)) == 0ull);
+        const uint64_t r = __ballot(me && (Cm & kept) != 0ull);
+        kept |= k;
+        undecided &= ~(k | r);
+      }
+      int nk = __popcll(kept);
+      bool done = false;
+      if (kept0 + nk >= max_det) {
+        const int allow = max_det - kept0;
+        uint64_t m = kept;
+        for (int i = 0; i < allow - 1; ++i) m &= m - 1ull;
+        const uint64_t last = m & (~m + 1ull);
+        kept &= (last << 1) - 1ull;
+        nk = allow;
+        done = true;
+      }
+      if ((kept >> lane) & 1ull) {
+        const int r = __popcll(kept & ((1ull << lane) - 1ull));
+        kbox[kept0 + r] = tile_box[lane];
+        karea[kept0 + r] = tile_area[lane];
+        kidx[kept0 + r] = tile_idx[lane];
+      }
+      if (lane == 0) {
+        s_nk = nk;
+        s_kept = kept0 + nk;
+        s_done = done ? 2 : (s_next >= M ? 1 : 0);
+      }
+    }
+    __syncthreads();
+    if (s_done) break;
+    const int start = s_next;
+    test_range(start, F, s_kept - s_nk, s_kept);
+    cursor = start;
+    __syncthreads();
+  }
+  for (int slot = threadIdx.x; slot < s_kept; slot += NMS2_G_THREADS) emit_det(kidx[slot], slot);
+  if (threadIdx.x == 0) counts[n] = s_kept;
+}
+
+static int nms2(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou,
+                int max_det, int max_nms, float max_wh, char* ws, size_t per, float* dets, int64_t* keep,
+                int32_t* counts, hipStream_t s, const NmsClassMask& cm) {
+  const int Mc = std::min(A, max_nms);
+  const int A2 = nms2_a2(A), nch = A2 / NMS2_CH;
+  const size_t lds = size_t((Mc + 15) & ~15) + size_t(max_det) * 24;
+  FCE_CHECK(lds <= 64 * 1024, "nms: greedy LDS over 64 KiB");
+  FCE_LAUNCH(nms2_keys_kernel, dim3(A2 / 256, n), dim3(256), 0, s, pred, best, nc, A, Mc, conf, ws, per, cm);
+  FCE_LAUNCH(nms2_sort_kernel, dim3(nch, n), dim3(NMS2_SORT_THREADS), 0, s, A, Mc, ws, per);
+  FCE_LAUNCH(nms2_rank_kernel, dim3(nch, n), dim3(256), 0, s, pred, nc, A, Mc, max_nms, max_wh, ws, per);
+  FCE_LAUNCH(nms2_greedy_kernel, dim3(n), dim3(NMS2_G_THREADS), lds, s, pred, nc, A, Mc, iou, max_det, max_nms, ws,
+             per, dets, keep, counts);
+  return launch_status("nms2_greedy_kernel");
+}
+
 int nms(const float* pred, const unsigned long long* best, int n, int nc, int A, float conf, float iou, int max_det,
         int max_nms, float max_wh, void* ws, size_t ws_bytes, float* dets, int64_t* keep, int32_t* counts,
         hipStream_t s, int multi, const int32_t* classes, int nclasses) {
@@ -704,6 +1102,11 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
   const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
   const int stop = stop_env ? atoi(stop_env) : 0;
   if (multi) best = nullptr;  // candidates come from every class row
+  const char* v1e = getenv("FCE_NMS_V1");  // the one-workgroup kernel (comparison runs)
+  const bool v1 = v1e && atoi(v1e) != 0;
+  if (!multi && A > 0 && max_det <= KEPT_CAP && !v1 && stop == 0)
+    return nms2(pred, best, n, nc, A, conf, iou, max_det, max_nms, max_wh, static_cast<char*>(ws), per, dets, keep,
+                counts, s, cm);
   if (A > 0 && !best && !multi)  // else the keys came from the Detect cls epilogue (fce_nms_best)
     FCE_LAUNCH(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);

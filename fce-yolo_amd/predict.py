@@ -156,7 +156,8 @@ class Predictor:
         self._next = (k + 1) % len(self.slots)
         sl = self.slots[k]
         if sl.ticket is not None:  # the slot's previous batch: collect it before its buffers are reused
-            self._ready[sl.ticket] = self._collect(sl)
+            t = sl.ticket
+            self._ready[t] = self._collect(sl)
         n = len(imgs)
         H, W = self.engine.H, self.engine.W
         db = self._desc_bytes()
