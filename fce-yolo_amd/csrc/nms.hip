@@ -685,7 +685,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
 }
 
 
-// ================================================================ multi-workgroup NMS (the default path)
+// ================================================================ multi-workgroup NMS (opt-in: FCE_NMS_V2=1)
 // The one-workgroup kernel above needs a whole CU per image (1024 threads, 112 KB of LDS), so beside the
 // forward of other batches it waits for CUs to drain, and its candidate and sort phases are serial over
 // one workgroup.  Here the same computation is four launches:
@@ -1102,8 +1102,9 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
   const char* stop_env = getenv("FCE_NMS_STOP");  // diagnostics: end the kernel after phase 1 / 2
   const int stop = stop_env ? atoi(stop_env) : 0;
   if (multi) best = nullptr;  // candidates come from every class row
-  const char* v1e = getenv("FCE_NMS_V1");  // the one-workgroup kernel (comparison runs)
-  const bool v1 = v1e && atoi(v1e) != 0;
+  // FCE_NMS_V2=1: the multi-workgroup path (opt-in: measured slower on the bench batch)
+  const char* v2e = getenv("FCE_NMS_V2");
+  const bool v1 = !(v2e && atoi(v2e) != 0);
   if (!multi && A > 0 && max_det <= KEPT_CAP && !v1 && stop == 0)
     return nms2(pred, best, n, nc, A, conf, iou, max_det, max_nms, max_wh, static_cast<char*>(ws), per, dets, keep,
                 counts, s, cm);

@@ -1,6 +1,5 @@
-"""Device NMS on the bench batch (n-fce 640 bs32 predictions of the seeded model): the multi-workgroup path
-(default) against the one-workgroup kernel (FCE_NMS_V1=1): bitwise-equal outputs, event-timed per call, alone
-and beside a concurrent forward on another stream.
+"""Device NMS on the bench batch (n-fce 640 bs32 predictions of the seeded model): the one-workgroup kernel
+(default) against the multi-workgroup path (FCE_NMS_V2=1): bitwise-equal outputs, event-timed per call.
 
     python scripts/nms_bench.py [--batch 32] [--imgsz 640] [--iters 50]
 """
@@ -50,30 +49,18 @@ def main():
     nms = NMS(a.batch, eng.anchors, eng.nc, dev)
     res = {}
     for mode in ("v2", "v1"):
-        if mode == "v1":
-            os.environ["FCE_NMS_V1"] = "1"
+        if mode == "v2":
+            os.environ["FCE_NMS_V2"] = "1"
         else:
-            os.environ.pop("FCE_NMS_V1", None)
+            os.environ.pop("FCE_NMS_V2", None)
         nms(pred, best)
         torch.cuda.synchronize()
         out = nms.buf.clone()
         t_keys = timed(lambda: nms(pred, best), a.iters)
         t_plain = timed(lambda: nms(pred), a.iters)
-        # beside a forward on another stream (what the lanes do)
-        side = torch.cuda.Stream(dev)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            with torch.cuda.stream(side):
-                eng(x)
-            nms(pred, best)
-        e1.record()
-        torch.cuda.synchronize()
-        both = e0.elapsed_time(e1) / 10
         res[mode] = out
-        print(f"{mode}: nms with keys {t_keys:.1f} us, with its own arg-max {t_plain:.1f} us, 10 x (forward on a side "
-              f"stream + nms) {both:.3f} ms per pair; kept per image {nms.counts[:4].tolist()}", flush=True)
+        print(f"{mode}: nms with keys {t_keys:.1f} us, with its own arg-max {t_plain:.1f} us; kept per image "
+              f"{nms.counts[:4].tolist()}", flush=True)
     print("v1 == v2 bitwise:", torch.equal(res["v1"], res["v2"]))
 
 

@@ -284,8 +284,16 @@ def test_640_matches_reference_digest(e2e_fx, device):
     assert np.abs(got[:, 4:] - ref[:, 4:]).max() <= CLS_TOL
 
 
+@pytest.fixture(params=["v1", "v2"])
+def nms_path(request, monkeypatch):
+    """Both device NMS paths: the one-workgroup kernel (default) and the multi-workgroup one (FCE_NMS_V2=1)."""
+    if request.param == "v2":
+        monkeypatch.setenv("FCE_NMS_V2", "1")
+    return request.param
+
+
 @pytest.mark.parametrize("name", ["designed_small", "designed_many", "none", "saturated_maxdet"])
-def test_nms_bit_exact_vs_reference(name, nms_fx, device):
+def test_nms_bit_exact_vs_reference(name, nms_fx, device, nms_path):
     fx = nms_fx.group(name)
     pred = torch.from_numpy(fx["pred"]).to(device)
     dets, keep = non_max_suppression(pred, 0.25, 0.7, 300, return_idxs=True)
@@ -295,7 +303,7 @@ def test_nms_bit_exact_vs_reference(name, nms_fx, device):
 
 
 @pytest.mark.parametrize("name", NMS_OPT_CASES)
-def test_nms_options_bit_exact_vs_reference(name, nms_opts_fx, device):
+def test_nms_options_bit_exact_vs_reference(name, nms_opts_fx, device, nms_path):
     """fce_nms_ex (classes / agnostic / multi_label, nms.py:116-141): kept anchors and rows bit-exact against the
     reference's outputs; with best-class keys built like the Detect epilogue's too (ignored by multi_label)."""
     pred, opts, exp = nms_opt_case(nms_opts_fx, name)
@@ -322,7 +330,7 @@ def test_nms_on_reference_model_output(e2e_fx, device):
         assert np.array_equal(dets[b].cpu().numpy(), fx[f"nms_det{b}"])
 
 
-def test_nms_on_gpu_predictions_matches_oracle(e2e_fx, device):
+def test_nms_on_gpu_predictions_matches_oracle(e2e_fx, device, nms_path):
     key = "yolo11n-fce_320_b1"
     fx = e2e_fx.group(key)
     _, _, _, y = _engine_run(key, fx, device)
@@ -333,7 +341,7 @@ def test_nms_on_gpu_predictions_matches_oracle(e2e_fx, device):
         assert np.array_equal(dets[0].cpu().numpy(), odets[0])
 
 
-def test_nms_large_candidate_set_global_sort(device):
+def test_nms_large_candidate_set_global_sort(device, nms_path):
     """> 8192 candidates takes the workspace (global-memory) bitonic sort path; max_nms truncation."""
     rng = np.random.default_rng(3)
     A = 33600
@@ -350,7 +358,7 @@ def test_nms_large_candidate_set_global_sort(device):
 
 
 @pytest.mark.parametrize("case", ["group_done", "group_runs_out", "group_is_everything"])
-def test_nms_equal_top_score_group(case, device):
+def test_nms_equal_top_score_group(case, device, nms_path):
     """>= max_det candidates share the top score (saturated sigmoids): ties resolved by anchor order, whether the
     greedy stops inside the tied group, runs through it (one pile of near-identical boxes), or the whole candidate
     set is tied.  Bit-exact vs the oracle."""
@@ -379,7 +387,7 @@ def test_nms_equal_top_score_group(case, device):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_nms_clustered_suppression_chains(seed, device):
+def test_nms_clustered_suppression_chains(seed, device, nms_path):
     """Heavy, chained suppression: jittered boxes around a few centres, few classes, tied (quantised)
     scores; several IoU thresholds and max_det values.  Kept indices and rows bit-exact vs the oracle."""
     rng = np.random.default_rng(100 + seed)
@@ -402,7 +410,7 @@ def test_nms_clustered_suppression_chains(seed, device):
 
 
 @pytest.mark.parametrize("case", ["bench_like", "unbanded", "one_class_heavy"])
-def test_nms_top_selection_and_class_buckets(case, device):
+def test_nms_top_selection_and_class_buckets(case, device, nms_path):
     """The large-candidate-set paths against the oracle: top-1024 selection (MSB radix select on tied
     scores) with the full-sort fallback, and the class-bucketed kept lists (exact only inside the class
     bands; `unbanded` breaks the band condition with max_wh below the box extent)."""
