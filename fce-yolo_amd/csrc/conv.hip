@@ -2375,6 +2375,11 @@ static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (rin
   return v;
 }
 
+static bool wide3_on() {  // read per call, like FCE_TILE3AL (the variant tests switch it on mid-process)
+  const char* e = getenv("FCE_WIDE3");
+  return e && atoi(e) != 0;
+}
+
 int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap) {
   if (is_stem(d)) return 0;
   if (is_dw(d)) {  // depthwise kernel variants, coded 100 + variant
@@ -2445,6 +2450,10 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int ab : {2, 3})
       for (int wm : {1, 2})
         if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
+  // wide tile (opt-in, FCE_WIDE3=1: measured at parity or slower on every m/l shape): 0xA00 | cwl << 4
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && wide3_on())
+    for (int cwl = 0; cwl < 3; ++cwl)
+      if (n < cap && wide3_ok(d.stride, 1 << cwl) && ((4 << cwl) >> 1) < cotiles) out[n++] = 0xA00 | (cwl << 4);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 128 && tile3al_on())  // A in LDS: | 1 << 15
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
@@ -2855,6 +2864,13 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
                   big3_ok(d.stride, wm, ab, nw),
               "conv: bad big-tile 3x3 hint");
     return launch_big3(a, wm, ab, nw, d.stride, x.n, s);
+  }
+  if (kind == 10) {  // wide-tile 3x3 kernel, per-K-step weight staging
+    const int cw = 1 << ((tile >> 4) & 3);
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xF) == 0 && (tile >> 6) == (0xA00 >> 6) &&
+                  wide3_ok(d.stride, cw),
+              "conv: bad wide-tile 3x3 hint");
+    return launch_wide3(a, cw, d.stride, x.n, s);
   }
   if (kind == 1) {  // LDS halo-tile 3x3 kernel
     rc = tile & 15;

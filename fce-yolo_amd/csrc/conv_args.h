@@ -116,5 +116,8 @@ static constexpr bool big3_ok(int s, int wm, int ab, int nw = 4) {
   return nw == 4 && (ab == 2 || ab == 3) && (s == 1 ? (wm == 1 || wm == 2) : wm == 2);
 }
 int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hipStream_t s);
+// Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
+bool wide3_ok(int stride, int cw);
+int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
 
 }  // namespace fce

@@ -627,9 +627,10 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
 @pytest.mark.parametrize("case", CONV_VARIANT_CASES)
 def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     """Every kernel variant the executor may autotune to (register tiles, LDS-tile kernels, the opt-in
-    A-in-LDS 3x3 tiles) gives the bit-identical result, and that result matches the fp64 reference
+    A-in-LDS and wide-tile 3x3 kernels) gives the bit-identical result, and that result matches the fp64 reference
     within the per-op tolerance."""
     monkeypatch.setenv("FCE_TILE3AL", "1")
+    monkeypatch.setenv("FCE_WIDE3", "1")  # + the opt-in wide-tile 3x3 (0xA00)
     cin, cout, k, stride, H, W, with_res = case
     g = torch.Generator().manual_seed(cin * 1000 + cout)
     w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
