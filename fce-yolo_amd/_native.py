@@ -148,6 +148,7 @@ _SIGS = {
     "fce_net_destroy": (None, [_P]),
     "fce_net_add_buffer": (_I, [_P, _I, _I, _I]),
     "fce_net_add_conv": (_I, [_P, _PCD, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "fce_net_add_conv_dup": (_I, [_P, _PCD, _I, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I]),
     "fce_net_add_maxpool_chain": (_I, [_P, _I, _I, _I, _I]),
     "fce_net_add_weighted_add": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I]),
     "fce_net_add_coord": (_I, [_P, _I, _PCO, _I, _I, _I, _I]),

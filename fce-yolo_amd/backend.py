@@ -246,10 +246,20 @@ class NetBackend:
         self.wadd(v, y, None, accumulate=0)
         return y
 
-    def conv(self, desc: N.ConvDesc, x: View, y: View, w_ptr: int, b_ptr: int, res: View | None = None):
+    supports_dup = True  # fce_net_add_conv_dup: a second, dense store of some output channels
+
+    def conv(self, desc: N.ConvDesc, x: View, y: View, w_ptr: int, b_ptr: int, res: View | None = None,
+             dup: tuple | None = None):
+        """`dup` = (dense View, first output channel): those output channels are also stored there."""
         desc.up = x.up
-        N.call("fce_net_add_conv", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff,
-               res.buf if res is not None else -1, res.coff if res is not None else 0, w_ptr, b_ptr)
+        args = (self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, res.buf if res is not None else -1,
+                res.coff if res is not None else 0, w_ptr, b_ptr)
+        if dup is None:
+            N.call("fce_net_add_conv", *args)
+        else:
+            dv, lo = dup
+            assert dv.coff == 0 and dv.c == dv.cstride
+            N.call("fce_net_add_conv_dup", *args, dv.buf, lo, dv.c)
 
     def maxpool_chain(self, buf: View, c: int, k: int):
         N.call("fce_net_add_maxpool_chain", self.net, buf.buf, buf.coff, c, k)

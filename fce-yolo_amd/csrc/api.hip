@@ -18,7 +18,7 @@ namespace fce {
 size_t conv_weight_bytes(const fce_conv_desc& d);
 int conv_pack(const fce_conv_desc& d, const float* w, void* out);
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s, int tile = -1);
+           const fce_tensor& y, hipStream_t s, int tile = -1, const fce_tensor* dup = nullptr, int duplo = 0);
 int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,
                   const fce_detect_epi& e, hipStream_t s, int tile = -1);
 int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out, int cap);
@@ -227,6 +227,7 @@ struct OpDesc {
   int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT
   fce_c3k2_desc c3k2{};              // OP_C3K2
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
+  int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
 };
 
 }  // namespace
@@ -350,6 +351,10 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
         r = net->view(op.res, op.res_coff, op.conv.cout);
         rp = &r;
       }
+      if (op.dup >= 0) {
+        const fce_tensor dv = net->view(op.dup, 0, op.dup_c);
+        return conv2d(op.conv, x, op.w, op.b, rp, y, s, op.tile, &dv, op.dup_lo);
+      }
       return conv2d(op.conv, x, op.w, op.b, rp, y, s, op.tile);
     }
     case OP_MAXPOOL: {
@@ -420,6 +425,7 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
       if (op.in >= 0) a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
       if (op.res >= 0) a.push_back({op.res, op.res_coff, op.res_coff + op.conv.cout, false});
       a.push_back({op.out, op.out_coff, op.out_coff + op.conv.cout, true});
+      if (op.dup >= 0) a.push_back({op.dup, 0, op.dup_c, true});
       break;
     case OP_MAXPOOL:
       a.push_back({op.in, op.in_coff, op.in_coff + op.in_c, false});
@@ -531,6 +537,7 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       const int osz = net->bufs[op.out].dtype == FCE_F32 ? 4 : 2;
       *bytes = N * ihw * d.cin * in_bytes + N * ohw * d.cout * osz + double(conv_weight_bytes(d));
       if (op.res >= 0) *bytes += N * ohw * d.cout * 2;
+      if (op.dup >= 0) *bytes += N * ohw * op.dup_c * 2;
       if (d.epilogue == FCE_EPI_ACCUM) *bytes += N * ohw * d.cout * 2;
       *flops = 2.0 * N * ohw * d.cout * d.k * d.k * (dw ? 1 : d.cin);
       break;
@@ -664,6 +671,22 @@ int fce_net_add_conv(fce_net* net, const fce_conv_desc* d, int in, int in_coff, 
   op.b = b;
   net->drop_graph();
   net->ops.push_back(op);
+  return FCE_OK;
+}
+
+int fce_net_add_conv_dup(fce_net* net, const fce_conv_desc* d, int in, int in_coff, int out, int out_coff, int res,
+                         int res_coff, const void* w, const float* b, int dup, int dup_lo, int dup_c) {
+  FCE_CHECK(net && valid_buf(net, dup, false) && dup_c > 0 && dup_c % 8 == 0 && dup_lo >= 0 && dup_lo % 8 == 0 &&
+                d && d->k == 1 && dup_lo + dup_c <= d->cout && net->bufs[dup].c == dup_c &&
+                net->bufs[dup].dtype == FCE_F16,
+            "fce_net_add_conv_dup: bad duplicate-store buffer or channel range");
+  const int st = fce_net_add_conv(net, d, in, in_coff, out, out_coff, res, res_coff, w, b);
+  if (st) return st;
+  OpDesc& op = net->ops.back();
+  FCE_CHECK(net->bufs[dup].shift == net->bufs[out].shift, "fce_net_add_conv_dup: dup buffer size differs");
+  op.dup = dup;
+  op.dup_lo = dup_lo;
+  op.dup_c = dup_c;
   return FCE_OK;
 }
 

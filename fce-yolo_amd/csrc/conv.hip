@@ -267,13 +267,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin((float)pv4[j] + fpin(alpha * v[j]));
         }
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+        const h4 hv = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+        *reinterpret_cast<h4*>(yo) = hv;
+        if (OUT == OUT_F16 && a.dup && co0 >= a.duplo && co0 < a.duplo + a.dupn)  // dupn % 8 == 0 (host)
+          *reinterpret_cast<h4*>(a.dup + int64_t(pix) * a.dupcs + (co0 - a.duplo)) = hv;
       } else {
         for (int j = 0; j < 4; ++j) {
           if (co0 + j >= a.cout) continue;
           float t = v[j];
           if (OUT == OUT_ACCUM) t = fpin((float)yo[j] + fpin(alpha * t));
           yo[j] = (_Float16)fpin(t);
+          if (OUT == OUT_F16 && a.dup && co0 + j >= a.duplo && co0 + j < a.duplo + a.dupn)
+            a.dup[int64_t(pix) * a.dupcs + (co0 + j - a.duplo)] = (_Float16)fpin(t);
         }
       }
     }
@@ -595,9 +600,12 @@ __device__ __forceinline__ void conv_store_staged(const ConvArgs& a, f4 (&acc)[R
     if (NP % 256 != 0 && e >= NP) break;
     const int px = e / NSL, sl = e - px * NSL;
     const int pix = pix0 + px, co = cbl0 * 16 + sl * 8;
-    if (pix < a.P && co < a.cout)
-      *reinterpret_cast<h8*>(static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co) =
-          *reinterpret_cast<const h8*>(ot + px * ROW + (sl ^ (px & (NSL - 1))) * 8);
+    if (pix < a.P && co < a.cout) {
+      const h8 hv = *reinterpret_cast<const h8*>(ot + px * ROW + (sl ^ (px & (NSL - 1))) * 8);
+      *reinterpret_cast<h8*>(static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co) = hv;
+      if (OUT == OUT_F16 && a.dup && co >= a.duplo && co < a.duplo + a.dupn)  // duplo, dupn % 8 == 0 (host)
+        *reinterpret_cast<h8*>(a.dup + int64_t(pix) * a.dupcs + (co - a.duplo)) = hv;
+    }
   }
 }
 
@@ -2607,7 +2615,8 @@ static int launch_ring3(const ConvArgs& a0, int rp, int stride, hipStream_t s) {
 }
 
 int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-                const fce_tensor& y, const fce_detect_epi* det, hipStream_t s, int tile) {
+                const fce_tensor& y, const fce_detect_epi* det, hipStream_t s, int tile, const fce_tensor* dup = nullptr,
+                int duplo = 0) {
   FCE_CHECK(d.k == 1 || d.k == 3 || (is_stem(d) && d.k <= 7), "conv: kernel size must be 1 or 3");
   FCE_CHECK(d.stride >= 1 && d.stride <= 2, "conv: stride must be 1 or 2");
   FCE_CHECK(x.n == y.n && x.c == d.cin && y.c == d.cout, "conv: channel/batch mismatch");
@@ -2814,6 +2823,18 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   a.det_w = Wo;
   a.det_stride = det ? det->stride : 0.f;
   a.det_best = det ? det->best : nullptr;
+  a.dup = nullptr;
+  a.dupcs = a.duplo = a.dupn = 0;
+  if (dup) {
+    FCE_CHECK(d.k == 1 && !is_dw(d) && out_kind == OUT_F16 && dup->layout == FCE_NHWC && dup->dtype == FCE_F16 &&
+                  dup->n == y.n && dup->h == Ho && dup->w == Wo && duplo >= 0 && duplo % 8 == 0 && dup->c % 8 == 0 &&
+                  duplo + dup->c <= d.cout && dup->cstride % 8 == 0 && dup->coff % 8 == 0 && a.vec_ok,
+              "conv: duplicate store needs a 1x1 fp16 plain store and 8-aligned channel ranges");
+    a.dup = static_cast<_Float16*>(dup->data) + dup->coff;
+    a.dupcs = dup->cstride;
+    a.duplo = duplo;
+    a.dupn = dup->c;
+  }
   const bool fast = d.cin % 32 == 0;
   int rc, rp;
   const int kind = tile >= 0 ? (tile >> 8) & 15 : -1;
@@ -2901,8 +2922,8 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
 }
 
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s, int tile) {
-  return conv2d_impl(d, x, w, bias, res, y, nullptr, s, tile);
+           const fce_tensor& y, hipStream_t s, int tile, const fce_tensor* dup, int duplo) {
+  return conv2d_impl(d, x, w, bias, res, y, nullptr, s, tile, dup, duplo);
 }
 
 int conv2d_detect(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias,

@@ -36,6 +36,11 @@ struct ConvArgs {
   int det_A, det_a0, det_nc, det_hw, det_w;
   float det_stride;
   unsigned long long* det_best;  // per-anchor best-class key [N][A] (fce_detect_epi::best), or null
+  // duplicate store (1x1, plain fp16 output): output channels [duplo, duplo + dupn) are also written to the
+  // dense view dup (dupcs channels per pixel), e.g. the half of a C2f cv1 output that the bottleneck reads,
+  // so it reads whole cache lines instead of a slice of the concat record; null = off
+  _Float16* dup;
+  int dupcs, duplo, dupn;
 };
 
 enum { OUT_F16 = 0, OUT_F32 = 1, OUT_WSTORE = 2, OUT_ACCUM = 3, OUT_DFL = 4, OUT_CLS = 5 };

@@ -19,7 +19,7 @@
 namespace fce {
 
 int conv2d(const fce_conv_desc& d, const fce_tensor& x, const void* w, const float* bias, const fce_tensor* res,
-           const fce_tensor& y, hipStream_t s, int tile = -1);
+           const fce_tensor& y, hipStream_t s, int tile = -1, const fce_tensor* dup = nullptr, int duplo = 0);
 
 enum { ACT_NONE_ = 0, ACT_SILU_ = 1, ACT_SIGMOID_ = 2 };
 

@@ -152,7 +152,7 @@ def _desc_copy(d: N.ConvDesc, **kw) -> N.ConvDesc:
 
 
 def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = None, res: View | None = None,
-              epilogue: int = N.EPI_STORE, fusion=None, out_dtype=N.F16) -> View:
+              epilogue: int = N.EPI_STORE, fusion=None, out_dtype=N.F16, dup=None) -> View:
     k, s = conv.kernel_size[0], conv.stride[0]
     ho = (x.h + 2 * (k // 2) - k) // s + 1
     wo = (x.w + 2 * (k // 2) - k) // s + 1
@@ -167,8 +167,18 @@ def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = No
         x = be.from_torch(x.buf) if isinstance(be, EagerBackend) else x
     if x.up and (k != 1 or conv.groups != 1):
         x = be.materialize(x)
-    be.conv(desc, x, y, nat.w.data_ptr(), nat.b.data_ptr(), res)
+    if dup is not None:
+        be.conv(desc, x, y, nat.w.data_ptr(), nat.b.data_ptr(), res, dup=dup)
+    else:
+        be.conv(desc, x, y, nat.w.data_ptr(), nat.b.data_ptr(), res)
     return y
+
+
+def _no_dup() -> bool:
+    """FCE_NO_DUP=1: C2f / C3k2 bottlenecks read their chunk from the concat record (no dense copy)."""
+    import os
+
+    return os.environ.get("FCE_NO_DUP", "0") not in ("", "0")
 
 
 def _backend(xs):
@@ -213,9 +223,9 @@ class Conv(nn.Module):
             return False
         raise NotImplementedError(f"fce_yolo_amd: activation {type(self.act).__name__} is not on the YOLO11 path")
 
-    def emit(self, be, x, out=None, res=None, epilogue=N.EPI_STORE, fusion=None, out_dtype=N.F16):
+    def emit(self, be, x, out=None, res=None, epilogue=N.EPI_STORE, fusion=None, out_dtype=N.F16, dup=None):
         return emit_conv(be, self.conv, getattr(self, "bn", None), self._act(), x, out, res, epilogue, fusion,
-                         out_dtype)
+                         out_dtype, dup)
 
     def forward(self, x):
         return _run_eager(self, x, keep_nchw=self.conv.in_channels <= 4)
@@ -298,9 +308,18 @@ class C2f(nn.Module):
     def emit(self, be, x, out=None):
         c, n = self.c, len(self.m)
         buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
-        self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
+        # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: whole-graph
+        # lowering also stores it densely from cv1's epilogue, so the block's 3x3 convs read whole cache lines
+        # (n32: ~1.5-2.3x the algorithmic bytes fetched through the slice)
+        dense = None
+        if getattr(be, "supports_dup", False) and n and c % 8 == 0 and not _no_dup():
+            dense = be.alloc(x.n, c, x.h, x.w)
+            self.cv1.emit(be, x, out=buf.slice(0, 2 * c), dup=(dense, c))
+        else:
+            self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
         for i, m in enumerate(self.m):
-            m.emit(be, buf.slice((1 + i) * c, c), out=buf.slice((2 + i) * c, c))
+            src = dense if (i == 0 and dense is not None) else buf.slice((1 + i) * c, c)
+            m.emit(be, src, out=buf.slice((2 + i) * c, c))
         return self.cv2.emit(be, buf, out=out)
 
     def forward(self, x):

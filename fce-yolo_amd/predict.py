@@ -79,6 +79,12 @@ class Letterbox:
         return self.out[: len(imgs)]
 
 
+# numpy images of the C structs (fce_letterbox_img: pointer + 7 ints, padded to 40 bytes; fce_box_scale)
+_LB_DT = np.dtype([("src", "<u8"), ("h0", "<i4"), ("w0", "<i4"), ("row_stride", "<i4"), ("new_h", "<i4"), ("new_w", "<i4"),
+                   ("top", "<i4"), ("left", "<i4"), ("pad", "<i4")])
+_BS_DT = np.dtype([("gain", "<f4"), ("pad_x", "<i4"), ("pad_y", "<i4"), ("h0", "<i4"), ("w0", "<i4")])
+
+
 class _Slot:
     """One batch in flight: pinned host staging (descriptors + packed source images), the device copy of it,
     the u8 canvas, an executor lane (own arena, own stream, captured hipGraph), NMS, pinned results."""
@@ -123,6 +129,8 @@ class Predictor:
 
     def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 3,
                  graph: bool = True, workers: int | None = None):
+        """`workers`: host threads packing images into pinned memory (default min(8, cpus / 2); 4-8 reach
+        ~31 GB/s on the MI355X box, scripts/predict_diag.py)."""
         import os
         from concurrent.futures import ThreadPoolExecutor
 
@@ -137,7 +145,9 @@ class Predictor:
         self.slots = [_Slot(e, batch, self.device, nms_kw) for e in engs]
         self.nms = self.slots[0].nms  # slot 0's NMS (API compatibility)
         self.lb = Letterbox(batch, (self.engine.H, self.engine.W), self.device)  # standalone use
-        self.pool = ThreadPoolExecutor(workers or max(1, min(8, (os.cpu_count() or 2) // 2)))
+        self.workers = workers or max(1, min(8, (os.cpu_count() or 2) // 2))
+        self.pool = ThreadPoolExecutor(self.workers)
+        self._geom = {}  # (h0, w0) -> (letterbox placement, box-scale parameters)
         self._next = 0
         self._ready = {}  # ticket -> results collected early (slot reused before result())
         self._tickets = 0
@@ -145,7 +155,10 @@ class Predictor:
     def _desc_bytes(self) -> int:
         return (self.batch * (C.sizeof(LetterboxImg) + C.sizeof(BoxScale)) + 255) // 256 * 256
 
-    def submit(self, images) -> int:
+    def _stage(self, images):
+        """Host half of a submit: pick the next slot (collecting its previous batch if still pending), build
+        the descriptors in its pinned buffer and start packing the images into it on the host thread pool.
+        Returns the staging record _issue consumes; the packing runs while the caller does other work."""
         if not 0 < len(images) <= self.batch:
             raise ValueError(f"Predictor: 1..{self.batch} images per call")
         imgs = [np.ascontiguousarray(im) for im in images]
@@ -161,30 +174,47 @@ class Predictor:
         n = len(imgs)
         H, W = self.engine.H, self.engine.W
         db = self._desc_bytes()
-        offs, off = [], db
-        for im in imgs:
-            offs.append(off)
-            off += (im.nbytes + 255) // 256 * 256
+        sizes = np.array([(im.nbytes + 255) // 256 * 256 for im in imgs], np.int64)
+        offs = db + np.concatenate(([0], np.cumsum(sizes)[:-1]))
+        off = int(db + sizes.sum())
         sl.reserve(off, self.device)
         sl.done.synchronize()  # (already collected above) the staging buffers are free
         hbase, dbase = sl.host.data_ptr(), sl.dev.data_ptr()
         hnp = sl.host.numpy()
-        futs = [self.pool.submit(np.copyto, hnp[o:o + im.nbytes].reshape(im.shape), im) for o, im in zip(offs, imgs)]
-        lbd = (LetterboxImg * n)()
-        scd = (BoxScale * self.batch)()
-        for i, im in enumerate(imgs):
-            h0, w0 = int(im.shape[0]), int(im.shape[1])
-            new_h, new_w, top, left = letterbox_geometry(h0, w0, H, W)
-            lbd[i] = LetterboxImg(dbase + offs[i], h0, w0, w0 * 3, new_h, new_w, top, left)
-        for i in range(self.batch):
-            h0, w0 = imgs[min(i, n - 1)].shape[:2]
-            gain, px, py = box_scale(H, W, int(h0), int(w0))
-            scd[i] = BoxScale(gain, px, py, int(h0), int(w0))
-        nlb = self.batch * C.sizeof(LetterboxImg)
-        C.memmove(hbase, lbd, C.sizeof(lbd))
-        C.memmove(hbase + nlb, scd, C.sizeof(scd))
+        # one packing task per worker (a contiguous run of images), not one per image
+        nw = min(self.workers, n)
+        bounds = [n * w // nw for w in range(nw + 1)]
+
+        def pack(lo, hi):
+            for i in range(lo, hi):
+                im = imgs[i]
+                np.copyto(hnp[offs[i]:offs[i] + im.nbytes].reshape(im.shape), im)
+
+        futs = [self.pool.submit(pack, bounds[w], bounds[w + 1]) for w in range(nw)]
+        # descriptors: letterbox placement and box scaling per distinct source shape (host, reference rounding)
+        lbd = np.zeros(n, _LB_DT)
+        scd = np.zeros(self.batch, _BS_DT)
+        shapes = [im.shape[:2] for im in imgs]
+        for i, (h0, w0) in enumerate(shapes):
+            g = self._geom.get((h0, w0))
+            if g is None:
+                g = self._geom[(h0, w0)] = (letterbox_geometry(h0, w0, H, W), box_scale(H, W, h0, w0))
+            (new_h, new_w, top, left), (gain, px, py) = g
+            lbd[i] = (dbase + int(offs[i]), h0, w0, w0 * 3, new_h, new_w, top, left, 0)
+            scd[i] = (gain, px, py, h0, w0)
+        scd[n:] = scd[n - 1]
+        C.memmove(hbase, lbd.ctypes.data, lbd.nbytes)
+        C.memmove(hbase + self.batch * C.sizeof(LetterboxImg), scd.ctypes.data, scd.nbytes)
+        return sl, futs, n, off, shapes
+
+    def _issue(self, staged) -> int:
+        """Device half: once the packing is done, one H2D copy and the whole chain on the slot's stream."""
+        sl, futs, n, off, shapes = staged
         for f in futs:
             f.result()
+        H, W = self.engine.H, self.engine.W
+        dbase = sl.dev.data_ptr()
+        nlb = self.batch * C.sizeof(LetterboxImg)
         main = torch.cuda.current_stream(self.device)
         sl.stream.wait_stream(main)
         with torch.cuda.stream(sl.stream):
@@ -201,15 +231,18 @@ class Predictor:
             sl.done.record(sl.stream)
         self._tickets += 1
         sl.ticket = self._tickets
-        sl.shapes = [im.shape[:2] for im in imgs]
+        sl.shapes = shapes
         return sl.ticket
+
+    def submit(self, images) -> int:
+        return self._issue(self._stage(images))
 
     def _collect(self, sl: _Slot):
         sl.done.synchronize()
-        keep, dets, counts = NMS.unpack(sl.out_host, self.batch, self.max_det)
+        keep, dets, counts = NMS.unpack(sl.out_host.clone(), self.batch, self.max_det)  # one copy out of pinned memory
         n = len(sl.shapes)
         cnt = counts[:n].tolist()
-        res = ([dets[i, :cnt[i]].clone() for i in range(n)], [keep[i, :cnt[i]].clone() for i in range(n)])
+        res = ([dets[i, :cnt[i]] for i in range(n)], [keep[i, :cnt[i]] for i in range(n)])
         sl.ticket = None
         return res
 
@@ -230,16 +263,26 @@ class Predictor:
         return self.result(self.submit(images), return_idxs)
 
     def stream(self, batches, return_idxs: bool = False):
-        """Generator over an iterable of image batches with `lanes` batches in flight (results in order)."""
+        """Generator over an iterable of image batches with `lanes` batches in flight, results in order.  Batch
+        i + 1 is staged (its images packed by the host pool into its slot) before batch i is issued, so the
+        packing overlaps the host's launches and the device work of the batches in flight."""
         from collections import deque
 
         q = deque()
-        for imgs in batches:
-            if len(q) == len(self.slots):
+        it = iter(batches)
+        if len(self.slots) < 2:  # one slot: staging ahead would overwrite the batch being issued
+            for imgs in it:
+                yield self(imgs, return_idxs)
+            return
+        nxt = next(it, None)
+        staged = self._stage(nxt) if nxt is not None else None
+        while staged is not None:
+            nxt = next(it, None)
+            ahead = self._stage(nxt) if nxt is not None else None  # may collect q[0] into _ready
+            q.append(self._issue(staged))
+            staged = ahead
+            while q and (len(q) >= len(self.slots) or staged is None or q[0] in self._ready):
                 yield self.result(q.popleft(), return_idxs)
-            q.append(self.submit(imgs))
-        while q:
-            yield self.result(q.popleft(), return_idxs)
 
     def close(self):
         torch.cuda.synchronize(self.device)

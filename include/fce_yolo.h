@@ -247,6 +247,13 @@ int fce_net_add_buffer(fce_net* net, int c, int shift, int dtype);
 /* ops reference buffers by id; channel slices by (coff, c).  -1 = the network input. */
 int fce_net_add_conv(fce_net* net, const fce_conv_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
                      int res_buf, int res_coff, const void* w_packed, const float* bias);
+/* fce_net_add_conv whose output channels [dup_lo, dup_lo + dup_c) are ALSO stored into buffer dup (exactly
+ * dup_c channels, same spatial size): a 1x1 conv with a plain fp16 store, 8-aligned channel ranges (ABI v5).
+ * The C2f / C3k2 lowering gives the chunk its bottlenecks read (block.py:303-307) a dense copy, so their 3x3
+ * convs read whole cache lines instead of a 16- or 32-channel slice of the concat record. */
+int fce_net_add_conv_dup(fce_net* net, const fce_conv_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
+                         int res_buf, int res_coff, const void* w_packed, const float* bias, int dup_buf, int dup_lo,
+                         int dup_c);
 int fce_net_add_maxpool_chain(fce_net* net, int buf, int in_coff, int c, int k);
 int fce_net_add_weighted_add(fce_net* net, int in_buf, int in_coff, int c, int up, const float* fusion_w,
                              int fusion_n, int fusion_i, int accumulate, int out_buf, int out_coff);

@@ -249,6 +249,24 @@ def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, device, monke
     assert torch.equal(u, f)
 
 
+@pytest.mark.parametrize("cfg,mut,batch,imgsz", [("yolo11n-fce.yaml", None, 2, 320), ("yolo11s-bifpn.yaml", None, 2, 256),
+                                                 ("yolo11m-fce.yaml", cases.heads8, 1, 256)])
+def test_c2f_dense_chunk_copy_bitwise(cfg, mut, batch, imgsz, device, monkeypatch):
+    """Whole-graph lowering stores the chunk a C2f / C3k2's first block reads densely from cv1's epilogue
+    (fce_net_add_conv_dup); the forward is bitwise the one that reads it as a slice of the concat record
+    (FCE_NO_DUP=1), and the dense copy equals that slice."""
+    model = cases.seeded_model(cfg, 0, mut).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(21)).half().to(device)
+    e1 = Engine(model, batch, imgsz, device)
+    y1 = e1(x).clone()
+    monkeypatch.setenv("FCE_NO_DUP", "1")
+    e0 = Engine(model, batch, imgsz, device)
+    y0 = e0(x).clone()
+    torch.cuda.synchronize()
+    assert e1.num_ops() == e0.num_ops() and e1.arena_bytes() > e0.arena_bytes()
+    assert torch.equal(y1, y0)
+
+
 @pytest.mark.parametrize("cfg,mut,batch,imgsz,rows", [
     ("yolo11n-fce.yaml", None, 32, 640, (0, 17, 31)),
     ("yolo11s-bifpn.yaml", None, 32, 640, (0, 31)),
