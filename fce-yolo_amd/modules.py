@@ -308,11 +308,12 @@ class C2f(nn.Module):
     def emit(self, be, x, out=None):
         c, n = self.c, len(self.m)
         buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
-        # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: whole-graph
-        # lowering also stores it densely from cv1's epilogue, so the block's 3x3 convs read whole cache lines
-        # (n32: ~1.5-2.3x the algorithmic bytes fetched through the slice)
+        # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: when that
+        # slice is narrower than a 128-byte line (c < 64), whole-graph lowering also stores it densely from cv1's
+        # epilogue, so the block's 3x3 convs read whole cache lines (n32: 1.5-2.3x the algorithmic bytes were
+        # fetched through the slice)
         dense = None
-        if getattr(be, "supports_dup", False) and n and c % 8 == 0 and not _no_dup():
+        if getattr(be, "supports_dup", False) and n and c % 8 == 0 and c < 64 and not _no_dup():
             dense = be.alloc(x.n, c, x.h, x.w)
             self.cv1.emit(be, x, out=buf.slice(0, 2 * c), dup=(dense, c))
         else:

@@ -85,9 +85,9 @@ _LB_DT = np.dtype([("src", "<u8"), ("h0", "<i4"), ("w0", "<i4"), ("row_stride", 
 _BS_DT = np.dtype([("gain", "<f4"), ("pad_x", "<i4"), ("pad_y", "<i4"), ("h0", "<i4"), ("w0", "<i4")])
 
 
-class _Slot:
-    """One batch in flight: pinned host staging (descriptors + packed source images), the device copy of it,
-    the u8 canvas, an executor lane (own arena, own stream, captured hipGraph), NMS, pinned results."""
+class _Lane:
+    """An executor lane: the u8 canvas, an Engine clone (own arena, own stream, its captured hipGraph), NMS and
+    the pinned host copy of its packed results."""
 
     def __init__(self, eng: Engine, batch: int, device, nms_kw):
         self.eng = eng
@@ -98,12 +98,21 @@ class _Slot:
         self.nms = NMS(batch, eng.anchors, eng.nc, device, **nms_kw)
         self.out_host = torch.empty(self.nms.buf.numel(), dtype=torch.uint8, pin_memory=True)
         self.done = torch.cuda.Event()
-        self.host = self.dev = None
-        self.ticket = None  # ticket whose results this slot holds (not yet collected)
+        self.ticket = None  # ticket whose results this lane holds (not yet collected)
         self.shapes = []
+
+
+class _Stage:
+    """A staging buffer: pinned host memory (descriptors + packed source images) and its device copy; `used`
+    is recorded once the letterbox has read the device copy, after which both may be refilled."""
+
+    def __init__(self):
+        self.host = self.dev = None
+        self.used = torch.cuda.Event()
 
     def reserve(self, nbytes: int, device):
         if self.host is None or self.host.numel() < nbytes:
+            self.used.synchronize()
             cap = max(nbytes, 1 << 20)
             cap += cap // 4  # headroom: a slightly larger batch of images does not re-pin
             self.host = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
@@ -116,16 +125,18 @@ class Predictor:
     The reference's predict loop (engine/predictor.py:151-182 preprocess, :276-381 stream_inference) as a
     pipeline of `lanes` batches in flight on the device.  `submit(images)` returns a ticket at once:
 
-      * the decoded uint8 HWC images are packed by a host thread pool into this slot's PINNED staging buffer
-        behind the letterbox / box-scale descriptors (built on the host exactly as LetterBox.__call__ and
-        ops.scale_boxes compute them), and go to the device in ONE async H2D copy on the slot's stream;
-      * device letterbox -> forward (the slot's executor lane replays its captured hipGraph) -> NMS with the
-        Detect epilogue's best-class keys -> scale_boxes, all on that stream;
+      * the decoded uint8 HWC images are packed by a host thread pool into a PINNED staging buffer behind the
+        letterbox / box-scale descriptors (built on the host exactly as LetterBox.__call__ and ops.scale_boxes
+        compute them), and go to the device in ONE async H2D copy;
+      * device letterbox -> forward (the lane's executor replays its captured hipGraph) -> NMS with the Detect
+        epilogue's best-class keys -> scale_boxes, all on the lane's stream;
       * the packed NMS outputs come back in one async D2H copy into pinned memory.
 
-    `result(ticket)` waits for that batch only and returns host tensors.  Slots are reused round-robin; a
-    slot's results not collected by then are kept on the host.  A call with fewer images than `batch`
-    repeats the last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
+    Staging buffers (lanes + 1 of them) are separate from the lanes: a buffer is free again as soon as the
+    letterbox of its batch has run, so `stream()` packs batch i + 1 while batches i - lanes + 1 .. i are on the
+    device.  `result(ticket)` waits for that batch only and returns host tensors; a lane's results not
+    collected when the lane is reused are kept on the host.  A call with fewer images than `batch` repeats the
+    last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
 
     def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 3,
                  graph: bool = True, workers: int | None = None):
@@ -142,108 +153,118 @@ class Predictor:
         engs = [self.engine] + [self.engine.clone() for _ in range(max(1, lanes) - 1)]
         for e in engs:
             e.graph = graph
-        self.slots = [_Slot(e, batch, self.device, nms_kw) for e in engs]
-        self.nms = self.slots[0].nms  # slot 0's NMS (API compatibility)
+        self.lanes = [_Lane(e, batch, self.device, nms_kw) for e in engs]
+        self.stages = [_Stage() for _ in range(len(self.lanes) + 1)]
+        self.nms = self.lanes[0].nms  # lane 0's NMS (API compatibility)
         self.lb = Letterbox(batch, (self.engine.H, self.engine.W), self.device)  # standalone use
         self.workers = workers or max(1, min(8, (os.cpu_count() or 2) // 2))
         self.pool = ThreadPoolExecutor(self.workers)
         self._geom = {}  # (h0, w0) -> (letterbox placement, box-scale parameters)
-        self._next = 0
-        self._ready = {}  # ticket -> results collected early (slot reused before result())
-        self._tickets = 0
+        self._n = 0  # batches staged so far
+        self._ready = {}  # ticket -> results collected early (lane reused before result())
 
     def _desc_bytes(self) -> int:
         return (self.batch * (C.sizeof(LetterboxImg) + C.sizeof(BoxScale)) + 255) // 256 * 256
 
     def _stage(self, images):
-        """Host half of a submit: pick the next slot (collecting its previous batch if still pending), build
-        the descriptors in its pinned buffer and start packing the images into it on the host thread pool.
-        Returns the staging record _issue consumes; the packing runs while the caller does other work."""
+        """Host half of a submit: the next staging buffer (waiting only for the letterbox of its previous
+        batch), descriptors written into it, and the packing of the images started on the host thread pool.
+        Returns the record _issue consumes; the packing runs while the caller does other work."""
         if not 0 < len(images) <= self.batch:
             raise ValueError(f"Predictor: 1..{self.batch} images per call")
         imgs = [np.ascontiguousarray(im) for im in images]
         for im in imgs:
             if im.dtype != np.uint8 or im.ndim != 3 or im.shape[2] != 3:
                 raise ValueError("Predictor: images must be uint8 (h, w, 3) BGR arrays")
-        k = self._next
-        self._next = (k + 1) % len(self.slots)
-        sl = self.slots[k]
-        if sl.ticket is not None:  # the slot's previous batch: collect it before its buffers are reused
-            t = sl.ticket
-            self._ready[t] = self._collect(sl)
+        i = self._n
+        self._n += 1
+        sb = self.stages[i % len(self.stages)]
         n = len(imgs)
         H, W = self.engine.H, self.engine.W
         db = self._desc_bytes()
         sizes = np.array([(im.nbytes + 255) // 256 * 256 for im in imgs], np.int64)
         offs = db + np.concatenate(([0], np.cumsum(sizes)[:-1]))
         off = int(db + sizes.sum())
-        sl.reserve(off, self.device)
-        sl.done.synchronize()  # (already collected above) the staging buffers are free
-        hbase, dbase = sl.host.data_ptr(), sl.dev.data_ptr()
-        hnp = sl.host.numpy()
+        sb.reserve(off, self.device)
+        sb.used.synchronize()  # the previous batch's letterbox has read this buffer
+        hbase, dbase = sb.host.data_ptr(), sb.dev.data_ptr()
+        hnp = sb.host.numpy()
         # one packing task per worker (a contiguous run of images), not one per image
         nw = min(self.workers, n)
         bounds = [n * w // nw for w in range(nw + 1)]
 
         def pack(lo, hi):
-            for i in range(lo, hi):
-                im = imgs[i]
-                np.copyto(hnp[offs[i]:offs[i] + im.nbytes].reshape(im.shape), im)
+            for j in range(lo, hi):
+                im = imgs[j]
+                np.copyto(hnp[offs[j]:offs[j] + im.nbytes].reshape(im.shape), im)
 
         futs = [self.pool.submit(pack, bounds[w], bounds[w + 1]) for w in range(nw)]
         # descriptors: letterbox placement and box scaling per distinct source shape (host, reference rounding)
         lbd = np.zeros(n, _LB_DT)
         scd = np.zeros(self.batch, _BS_DT)
         shapes = [im.shape[:2] for im in imgs]
-        for i, (h0, w0) in enumerate(shapes):
+        for j, (h0, w0) in enumerate(shapes):
             g = self._geom.get((h0, w0))
             if g is None:
                 g = self._geom[(h0, w0)] = (letterbox_geometry(h0, w0, H, W), box_scale(H, W, h0, w0))
             (new_h, new_w, top, left), (gain, px, py) = g
-            lbd[i] = (dbase + int(offs[i]), h0, w0, w0 * 3, new_h, new_w, top, left, 0)
-            scd[i] = (gain, px, py, h0, w0)
+            lbd[j] = (dbase + int(offs[j]), h0, w0, w0 * 3, new_h, new_w, top, left, 0)
+            scd[j] = (gain, px, py, h0, w0)
         scd[n:] = scd[n - 1]
         C.memmove(hbase, lbd.ctypes.data, lbd.nbytes)
         C.memmove(hbase + self.batch * C.sizeof(LetterboxImg), scd.ctypes.data, scd.nbytes)
-        return sl, futs, n, off, shapes
+        return i, sb, futs, n, off, shapes
 
     def _issue(self, staged) -> int:
-        """Device half: once the packing is done, one H2D copy and the whole chain on the slot's stream."""
-        sl, futs, n, off, shapes = staged
+        """Device half: lane i % lanes (its previous results collected first), once the packing is done one H2D
+        copy and the whole chain on the lane's stream.  Returns the ticket."""
+        i, sb, futs, n, off, shapes = staged
+        ln = self.lanes[i % len(self.lanes)]
+        if ln.ticket is not None:  # the lane's previous batch: collect it before its buffers are reused
+            t = ln.ticket
+            self._ready[t] = self._collect(ln)
         for f in futs:
             f.result()
         H, W = self.engine.H, self.engine.W
-        dbase = sl.dev.data_ptr()
+        dbase = sb.dev.data_ptr()
         nlb = self.batch * C.sizeof(LetterboxImg)
         main = torch.cuda.current_stream(self.device)
-        sl.stream.wait_stream(main)
-        with torch.cuda.stream(sl.stream):
-            sl.dev[:off].copy_(sl.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
-            st = sl.stream.cuda_stream
-            N.call("fce_letterbox", C.c_void_p(dbase), n, C.c_void_p(sl.canvas.data_ptr()), H, W, self.lb.pad, st)
+        ln.stream.wait_stream(main)
+        with torch.cuda.stream(ln.stream):
+            sb.dev[:off].copy_(sb.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
+            st = ln.stream.cuda_stream
+            N.call("fce_letterbox", C.c_void_p(dbase), n, C.c_void_p(ln.canvas.data_ptr()), H, W, self.lb.pad, st)
+            # the box-scale descriptors are read by scale_boxes below: copy them out before the buffer is freed
+            sc = self._scales_dev(ln)
+            sc.copy_(sb.dev[nlb:nlb + sc.numel()])
+            sb.used.record(ln.stream)
             if n < self.batch:  # fixed-shape engine: pad the batch by repeating the last canvas
-                sl.canvas[n:].copy_(sl.canvas[n - 1:n].expand(self.batch - n, -1, -1, -1))
-            sl.eng(sl.canvas, out=sl.pred, best=sl.best)
-            dets, keep, counts = sl.nms(sl.pred, sl.best)
+                ln.canvas[n:].copy_(ln.canvas[n - 1:n].expand(self.batch - n, -1, -1, -1))
+            ln.eng(ln.canvas, out=ln.pred, best=ln.best)
+            dets, keep, counts = ln.nms(ln.pred, ln.best)
             N.call("fce_scale_boxes", C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()), self.batch,
-                   self.max_det, C.c_void_p(dbase + nlb), st)
-            sl.out_host.copy_(sl.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
-            sl.done.record(sl.stream)
-        self._tickets += 1
-        sl.ticket = self._tickets
-        sl.shapes = shapes
-        return sl.ticket
+                   self.max_det, C.c_void_p(sc.data_ptr()), st)
+            ln.out_host.copy_(ln.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
+            ln.done.record(ln.stream)
+        ln.ticket = i + 1
+        ln.shapes = shapes
+        return ln.ticket
+
+    def _scales_dev(self, ln: _Lane) -> torch.Tensor:
+        if not hasattr(ln, "scales"):
+            ln.scales = torch.empty(self.batch * C.sizeof(BoxScale), dtype=torch.uint8, device=self.device)
+        return ln.scales
 
     def submit(self, images) -> int:
         return self._issue(self._stage(images))
 
-    def _collect(self, sl: _Slot):
-        sl.done.synchronize()
-        keep, dets, counts = NMS.unpack(sl.out_host.clone(), self.batch, self.max_det)  # one copy out of pinned memory
-        n = len(sl.shapes)
+    def _collect(self, ln: _Lane):
+        ln.done.synchronize()
+        keep, dets, counts = NMS.unpack(ln.out_host.clone(), self.batch, self.max_det)  # one copy out of pinned memory
+        n = len(ln.shapes)
         cnt = counts[:n].tolist()
         res = ([dets[i, :cnt[i]] for i in range(n)], [keep[i, :cnt[i]] for i in range(n)])
-        sl.ticket = None
+        ln.ticket = None
         return res
 
     def result(self, ticket: int, return_idxs: bool = False):
@@ -251,10 +272,10 @@ class Predictor:
         if ticket in self._ready:
             d, k = self._ready.pop(ticket)
         else:
-            sl = next((s for s in self.slots if s.ticket == ticket), None)
-            if sl is None:
+            ln = next((x for x in self.lanes if x.ticket == ticket), None)
+            if ln is None:
                 raise KeyError(f"Predictor: unknown or already collected ticket {ticket}")
-            d, k = self._collect(sl)
+            d, k = self._collect(ln)
         return (d, k) if return_idxs else d
 
     def __call__(self, images, return_idxs: bool = False):
@@ -264,28 +285,24 @@ class Predictor:
 
     def stream(self, batches, return_idxs: bool = False):
         """Generator over an iterable of image batches with `lanes` batches in flight, results in order.  Batch
-        i + 1 is staged (its images packed by the host pool into its slot) before batch i is issued, so the
-        packing overlaps the host's launches and the device work of the batches in flight."""
+        i + 1 is staged (its images packed by the host pool) before batch i is issued, so the packing overlaps
+        the host's launches and the device work of the batches in flight."""
         from collections import deque
 
         q = deque()
         it = iter(batches)
-        if len(self.slots) < 2:  # one slot: staging ahead would overwrite the batch being issued
-            for imgs in it:
-                yield self(imgs, return_idxs)
-            return
         nxt = next(it, None)
         staged = self._stage(nxt) if nxt is not None else None
         while staged is not None:
             nxt = next(it, None)
-            ahead = self._stage(nxt) if nxt is not None else None  # may collect q[0] into _ready
-            q.append(self._issue(staged))
+            ahead = self._stage(nxt) if nxt is not None else None
+            q.append(self._issue(staged))  # may collect q[0] into _ready (its lane is reused)
             staged = ahead
-            while q and (len(q) >= len(self.slots) or staged is None or q[0] in self._ready):
+            while q and (len(q) >= len(self.lanes) or staged is None or q[0] in self._ready):
                 yield self.result(q.popleft(), return_idxs)
 
     def close(self):
         torch.cuda.synchronize(self.device)
         self.pool.shutdown()
-        for s in self.slots:
-            s.eng.close()
+        for ln in self.lanes:
+            ln.eng.close()
