@@ -118,6 +118,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     ap.add_argument("--profile-passes", type=int, default=10, help="per-op HIP-event passes averaged")
+    ap.add_argument("--predict-lanes", type=int, default=5, help="batches in flight in the host-image predict leg")
     ap.add_argument("--predict-steps", type=int, default=30,
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
     a = ap.parse_args()
@@ -145,7 +146,7 @@ def predict_rate(model, B: int, S: int, dev, steps: int, lanes: int = 3):
 
     from fce_yolo_amd.predict import Predictor
 
-    pred = Predictor(model, B, S, dev, lanes=lanes)
+    pred = Predictor(model, B, S, dev, lanes=lanes, workers=4)
     rng = np.random.default_rng(0)
     batches = [[rng.integers(0, 256, (480, 640, 3), dtype=np.uint8) for _ in range(B)] for _ in range(2)]
     for _ in pred.stream([batches[i % 2] for i in range(2 * lanes)]):
@@ -161,8 +162,8 @@ def predict_rate(model, B: int, S: int, dev, steps: int, lanes: int = 3):
     pred.close()
     return {"images_per_sec": round(B * steps / el, 2), "ms_per_batch": round(el / steps * 1e3, 3),
             "batches_in_flight": lanes,
-            "source": f"{B} x 480x640 uint8 BGR host numpy images per batch, packed into pinned staging by host "
-                      f"threads, one async H2D per batch, device letterbox to {S}x{S} + forward (hipGraph lane) + NMS + "
+            "source": f"{B} x 480x640 uint8 BGR host numpy images per batch, packed into pinned staging by 4 host "
+                      f"threads, one async H2D per batch on a copy stream, device letterbox to {S}x{S} + forward (hipGraph lane) + NMS + "
                       f"scale_boxes, one async D2H of the detections, per-image results as host tensors; {steps} "
                       f"batches, predict.Predictor.stream"}
 
@@ -401,7 +402,7 @@ def main():
     if a.profile_json and rank == 0:
         Path(a.profile_json).write_text(json.dumps([list(p) for p in prof], indent=0))
     if rank == 0 and world == 1 and a.predict_steps > 0:
-        out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps, max(1, a.lanes))
+        out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps, a.predict_lanes)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds, B)
     elif rank == 0:

@@ -175,10 +175,12 @@ def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = No
 
 
 def _no_dup() -> bool:
-    """FCE_NO_DUP=1: C2f / C3k2 bottlenecks read their chunk from the concat record (no dense copy)."""
+    """C2f / C3k2 bottlenecks read their chunk from the concat record unless FCE_DUP=1 (dense copy from cv1's
+    epilogue): measured on n32 the copy takes ~20 us off the 3x3 family and puts ~20 us onto the 1x1 family
+    (forward 1.567-1.583 ms either way), so it stays opt-in."""
     import os
 
-    return os.environ.get("FCE_NO_DUP", "0") not in ("", "0")
+    return os.environ.get("FCE_DUP", "0") in ("", "0")
 
 
 def _backend(xs):
@@ -309,9 +311,9 @@ class C2f(nn.Module):
         c, n = self.c, len(self.m)
         buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
         # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: when that
-        # slice is narrower than a 128-byte line (c < 64), whole-graph lowering also stores it densely from cv1's
-        # epilogue, so the block's 3x3 convs read whole cache lines (n32: 1.5-2.3x the algorithmic bytes were
-        # fetched through the slice)
+        # slice is narrower than a 128-byte line (c < 64), whole-graph lowering can also store it densely from
+        # cv1's epilogue (FCE_DUP=1), so the block's 3x3 convs read whole cache lines (n32: 1.5-2.3x the
+        # algorithmic bytes are fetched through the slice)
         dense = None
         if getattr(be, "supports_dup", False) and n and c % 8 == 0 and c < 64 and not _no_dup():
             dense = be.alloc(x.n, c, x.h, x.w)

@@ -138,10 +138,12 @@ class Predictor:
     collected when the lane is reused are kept on the host.  A call with fewer images than `batch` repeats the
     last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
 
-    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 3,
-                 graph: bool = True, workers: int | None = None):
-        """`workers`: host threads packing images into pinned memory (default min(8, cpus / 2); 4-8 reach
-        ~31 GB/s on the MI355X box, scripts/predict_diag.py)."""
+    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 5,
+                 graph: bool = True, workers: int | None = None, copy_stream: bool = True):
+        """`lanes`: batches on the device at once (5: measured best for 32 x 480x640 images, scripts/predict_diag.py).
+        `workers`: host threads packing images into pinned memory (default min(8, cpus / 2); 4-8 reach ~31 GB/s
+        on the MI355X box).  `copy_stream` (default): every H2D copy on one dedicated stream, lanes wait on it
+        (18.9k against 15.9k images/s with the copy on the lane's own stream, scripts/predict_diag.py)."""
         import os
         from concurrent.futures import ThreadPoolExecutor
 
@@ -154,6 +156,7 @@ class Predictor:
         for e in engs:
             e.graph = graph
         self.lanes = [_Lane(e, batch, self.device, nms_kw) for e in engs]
+        self.copy = torch.cuda.Stream(self.device) if copy_stream else None
         self.stages = [_Stage() for _ in range(len(self.lanes) + 1)]
         self.nms = self.lanes[0].nms  # lane 0's NMS (API compatibility)
         self.lb = Letterbox(batch, (self.engine.H, self.engine.W), self.device)  # standalone use
@@ -230,8 +233,14 @@ class Predictor:
         nlb = self.batch * C.sizeof(LetterboxImg)
         main = torch.cuda.current_stream(self.device)
         ln.stream.wait_stream(main)
+        if self.copy is not None:
+            self.copy.wait_stream(main)
+            with torch.cuda.stream(self.copy):
+                sb.dev[:off].copy_(sb.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
+            ln.stream.wait_stream(self.copy)
         with torch.cuda.stream(ln.stream):
-            sb.dev[:off].copy_(sb.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
+            if self.copy is None:
+                sb.dev[:off].copy_(sb.host[:off], non_blocking=True)  # descriptors + images: one H2D copy
             st = ln.stream.cuda_stream
             N.call("fce_letterbox", C.c_void_p(dbase), n, C.c_void_p(ln.canvas.data_ptr()), H, W, self.lb.pad, st)
             # the box-scale descriptors are read by scale_boxes below: copy them out before the buffer is freed

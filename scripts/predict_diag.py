@@ -59,9 +59,13 @@ def main():
     model = DetectionModel("yolo11n-fce.yaml")
     model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
     model.eval().to(dev)
-    batches = [imgs, imgs[::-1]]
-    for lanes, workers in ((3, 8), (4, 8), (5, 8), (4, 4)):
-        p = Predictor(model, B, 640, dev, lanes=lanes, workers=workers)
+    for lanes, workers, cs, tiny in ((3, 8, False, False), (5, 8, False, False), (5, 4, False, False),
+                                     (5, 4, True, False), (6, 4, False, False), (5, 4, False, True)):
+        p = Predictor(model, B, 640, dev, lanes=lanes, workers=workers, copy_stream=cs)
+        if tiny:  # 32x32 sources: no packing / PCIe cost to speak of
+            batches = [[im[:32, :32].copy() for im in imgs]] * 2
+        else:
+            batches = [imgs, imgs[::-1]]
         for _ in p.stream([batches[i % 2] for i in range(2 * lanes)]):
             pass
         torch.cuda.synchronize()
@@ -81,8 +85,8 @@ def main():
                 p.result(q.pop(0))
         for t in q:
             p.result(t)
-        print(f"Predictor lanes {lanes} workers {workers}: {n / el:.0f} images/s ({el / 30 * 1e3:.2f} ms per batch; "
-              f"submit() {ts / 6 * 1e3:.2f} ms)", flush=True)
+        print(f"Predictor lanes {lanes} workers {workers} copy_stream {cs}{' 32x32 sources' if tiny else ''}: "
+              f"{n / el:.0f} images/s ({el / 30 * 1e3:.2f} ms per batch; submit() {ts / 6 * 1e3:.2f} ms)", flush=True)
         p.close()
 
 
