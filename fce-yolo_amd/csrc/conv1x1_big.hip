@@ -1,0 +1,155 @@
+// Big-tile 1x1 convolution: the wide pointwise convs of the m/l scales as a GEMM with 256 x 256 block tiles.
+// Replaces (reference, ultralytics/): nn/modules/conv.py:39-89 Conv.forward_fuse for 1x1 kernels (BN folded by
+// utils/torch_utils.py:237-267), the C2f / C3k / SPPF / C2PSA cv1 / cv2 / FFN pointwise convs, the BiFPN
+// realign convs (fce_block.py:24-38) and nn.Upsample feeding a 1x1 conv.  Variant code 0xB00 | log2(wc) << 4.
+//
+// A block is 8 waves (512 threads): WC waves along the couts, each owning 8 cout tiles (128 couts), times 8 / WC
+// waves along the pixels, each owning 4 groups of 16 pixels (64 pixels): every wave runs 32 MFMAs per K-step from
+// 8 A + 4 B fragment reads (0.375 KiB of LDS reads per MFMA, against 0.5 for 64 x 64 wave tiles), and the block
+// stages 16 KiB of weights + 16 KiB of pixels per K-step.  The copies go global -> LDS by LDS-DMA
+// (global_load_lds) into a ring of 4 K-step slots, issued 3 steps ahead: 96 KiB in flight per CU, which a
+// register-staged version (one step ahead, 32 KiB in flight: measured ~2.6 TB/s effective, Little's law at HBM
+// latency) could not reach without spilling.  One barrier per step, counted vmcnt waits.
+// Same K order (32-channel steps, ascending), same fragments and the shared epilogue (bias, SiLU, residual,
+// BiFPN weighted store / accumulate, Detect cls): bitwise identical to every other 1x1 variant.
+#include "conv_args.h"
+
+namespace fce {
+
+template <int WC>
+struct Big1Geom {
+  static constexpr int WP = 8 / WC;
+  static constexpr int BC = WC * 8;     // cout tiles per block
+  static constexpr int BP = WP * 64;    // pixels per block
+  static constexpr int NA = BC * 64;    // A pieces (16 B) per K-step = BC DMA instructions (1 KiB each)
+  static constexpr int NB = BP * 4;     // B pieces per K-step = NB / 64 DMA instructions
+  static constexpr int IA = BC / 8, IB = NB / 64 / 8;  // DMA instructions per wave per K-step
+  static constexpr int RING = 4;        // K-step slots: the copies of step s + 3 go out while step s computes
+  static constexpr size_t lds = size_t(RING) * (NA + NB) * 16;
+};
+
+__device__ __forceinline__ int b1_slot(int u, int q) { return u * 4 + (q ^ ((u >> 1) & 3)); }
+
+__device__ __forceinline__ void b1_glds16(const void* src, h8* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
+}
+
+template <int WC, int OUT>
+__global__ __launch_bounds__(512, 1) void conv1x1_big_kernel(ConvArgs a) {
+  using G = Big1Geom<WC>;
+  constexpr int WP = G::WP, BC = G::BC, BP = G::BP, NA = G::NA, NB = G::NB, IA = G::IA, IB = G::IB, RING = G::RING;
+  extern __shared__ __attribute__((aligned(16))) h8 big1_smem[];  // RING x [A | B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int wc = wave / WP, wp = wave - wc * WP;
+  // XCD-aware order (tile_block): the cout groups of one pixel tile land on one XCD's L2
+  int pt, cog;
+  tile_block(a.gy, pt, cog);
+  const int p0 = pt * BP;
+  const int cotiles = (a.cout + 15) >> 4;
+  const int ct_blk = cog * BC;
+  const int nst = (a.cin + 31) >> 5;
+  const h8* wts = reinterpret_cast<const h8*>(a.w);
+
+  // LDS-DMA copies (global_load_lds: no staging registers, no ds_write): this wave's instructions i = wave + 8 j.
+  // A instruction i = block cout tile i, lane l -> LDS slot 64 i + l (the fragment-read layout).  B instruction i
+  // covers LDS slots 64 i .. 64 i + 63 lane-linearly, so the XOR swizzle is applied to the SOURCE: slot e holds
+  // piece (e & 3) ^ ((u >> 1) & 3) of pixel u = e >> 2 (b1_slot is an involution on the piece index).
+  const h8* asrc[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int ct = min(ct_blk + wave + 8 * j, cotiles - 1);
+    asrc[j] = wts + size_t(ct) * a.nalloc * 64 + lane;
+  }
+  int64_t boff[IB];
+  int bq[IB];
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int e = (wave + 8 * j) * 64 + lane;
+    const int u = e >> 2, q = (e & 3) ^ ((u >> 1) & 3), pix = p0 + u;
+    boff[j] = pix < a.P ? conv1x1_src(a, pix) + q * 8 : -1;
+    bq[j] = q * 8;
+  }
+  auto issue = [&](int t) {  // step t's copies into ring slot t % RING
+    h8* slot = big1_smem + (t % RING) * (NA + NB);
+#pragma unroll
+    for (int j = 0; j < IA; ++j) b1_glds16(asrc[j] + size_t(t) * 64, slot + (wave + 8 * j) * 64);  // zero steps past nst
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const bool ok = boff[j] >= 0 && t * 32 + bq[j] < a.cin;
+      b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + t * 32) : static_cast<const void*>(g_zero_line),
+                slot + NA + (wave + 8 * j) * 64);
+    }
+  };
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: steps 0 .. RING - 2 in flight (copies past nst read zero weight steps / zero pixels: harmless)
+#pragma unroll
+  for (int t = 0; t < RING - 1; ++t) issue(t);
+  for (int s = 0; s < nst; ++s) {
+    // this wave's copies of step s have landed once only the (RING - 2) later steps' remain outstanding
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (IA + IB)) : "memory");
+    __syncthreads();  // every wave's copies of step s visible; step s - 1's reads done (slot (s - 1) % RING free)
+    issue(s + RING - 1);
+    const h8* cur = big1_smem + (s % RING) * (NA + NB);
+    const h8* As = cur + (wc * 8) * 64 + lane;
+    const h8* Bs = cur + NA;
+    h8 bf[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) bf[p] = Bs[b1_slot(wp * 64 + p * 16 + col, grp)];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const h8 af = As[r * 64];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[p], acc[r][p], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no copy may land after the block exits
+  conv_epilogue<8, 4, OUT>(a, acc, p0 + wp * 64, ct_blk + wc * 8, col, grp);
+}
+
+bool big1_ok(int wc) { return wc == 1 || wc == 2; }
+
+template <int WC, int OUT>
+static int launch_big1_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
+  constexpr size_t lds = Big1Geom<WC>::lds;
+  static_assert(lds <= 160 * 1024, "big 1x1 tile: LDS over 160 KiB");
+  static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_big_kernel<WC, OUT>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!big) return fail(FCE_ERR_HIP, "conv 1x1 big tile: cannot opt in to >64 KiB LDS");
+  FCE_LAUNCH((conv1x1_big_kernel<WC, OUT>), grid, dim3(512), lds, s, a);
+  return FCE_OK;
+}
+
+template <int WC>
+static int launch_big1_w(const ConvArgs& a, int out_kind, dim3 grid, hipStream_t s) {
+  switch (out_kind) {
+    case OUT_F16: return launch_big1_k<WC, OUT_F16>(a, grid, s);
+    case OUT_F32: return launch_big1_k<WC, OUT_F32>(a, grid, s);
+    case OUT_WSTORE: return launch_big1_k<WC, OUT_WSTORE>(a, grid, s);
+    case OUT_ACCUM: return launch_big1_k<WC, OUT_ACCUM>(a, grid, s);
+    case OUT_CLS: return launch_big1_k<WC, OUT_CLS>(a, grid, s);
+    default: return fail(FCE_ERR_INVALID, "conv 1x1 big tile: unsupported epilogue");
+  }
+}
+
+int launch_big1(const ConvArgs& a0, int out_kind, int wc, hipStream_t s) {
+  FCE_CHECK(big1_ok(wc) && a0.cin % 8 == 0 && out_kind != OUT_DFL, "conv 1x1 big tile: bad configuration");
+  ConvArgs a = a0;
+  const int bp = (8 / wc) * 64, bc = wc * 8;
+  a.gy = ((a.cout + 15) / 16 + bc - 1) / bc;
+  const int64_t tiles = (int64_t(a.P) + bp - 1) / bp;
+  FCE_CHECK(tiles * a.gy < (int64_t(1) << 31), "conv 1x1 big tile: grid too large");
+  const dim3 grid(unsigned(tiles * a.gy));
+  const int rc = wc == 1 ? launch_big1_w<1>(a, out_kind, grid, s) : launch_big1_w<2>(a, out_kind, grid, s);
+  if (rc != FCE_OK) return rc;
+  return launch_status("conv1x1_big_kernel");
+}
+
+}  // namespace fce

@@ -114,6 +114,180 @@ __device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP]
   }
 }
 
+// Epilogue of the dense MFMA kernels: acc[r][p] = 16 couts (cout tile cot0 + r) x 16 pixels
+// (pix_base + 16 p ..) of this wave; lane = (col = pixel, grp = 4-cout group).  Bias, SiLU, residual,
+// BiFPN weighted store / accumulate, or the fused Detect DFL / cls-sigmoid tails.
+template <int RC, int RP, int OUT>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][RP], int pix_base, int cot0, int col,
+                                              int grp) {
+  const int cotiles = (a.cout + 15) >> 4;
+  if (OUT == OUT_DFL) {
+    // Detect box branch (head.py:161-162, block.py:76-79, tal.py:367-376): the 4 x 16 logits of a
+    // pixel live in tiles r = side, lanes {p, p+16, p+32, p+48} x 4 registers -> softmax expectation
+    // with two xor-shuffles, then xywh * stride into pred rows 0..3 (fp32 throughout).
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      float dist[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v[4], mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[r < RC ? r : 0][p][j] + a.bias[r * 16 + grp * 4 + j];
+          mx = fmaxf(mx, v[j]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float den = 0.f, num = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float e = expf(v[j] - mx);
+          den += e;
+          num = __fadd_rn(num, __fmul_rn(e, (float)(grp * 4 + j)));  // no FMA: match detect_decode
+        }
+        den += __shfl_xor(den, 16);
+        den += __shfl_xor(den, 32);
+        num += __shfl_xor(num, 16);
+        num += __shfl_xor(num, 32);
+        dist[r] = num / den;
+      }
+      const int pix = pix_base + p * 16 + col;
+      if (grp == 0 && pix < a.P) {
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        const float ax = (float)(q % a.det_w) + 0.5f, ay = (float)(q / a.det_w) + 0.5f;
+        const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
+        float* o = a.pred + int64_t(n) * (4 + a.det_nc) * a.det_A + a.det_a0 + q;
+        if (a.det_best) a.det_best[int64_t(n) * a.det_A + a.det_a0 + q] = 0ull;  // the cls epilogue maxes into it
+        o[0] = (x1 + x2) / 2.0f * a.det_stride;
+        o[a.det_A] = (y1 + y2) / 2.0f * a.det_stride;
+        o[int64_t(2) * a.det_A] = (x2 - x1) * a.det_stride;
+        o[int64_t(3) * a.det_A] = (y2 - y1) * a.det_stride;
+      }
+    }
+    return;
+  }
+  if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
+    // with det_best: the pixel's best class over this wave's couts (first maximum, like torch.max in
+    // utils/nms.py) as one key = score bits << 32 | ~class (scores >= 0: integer order = float order;
+    // ties -> the lower class), merged over the 4 cout groups by xor-shuffles, one atomic max per pixel
+    unsigned long long bk[RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) bk[p] = 0ull;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+      const int co0 = (cot0 + r) * 16 + grp * 4;
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        const int pix = pix_base + p * 16 + col;
+        if (pix >= a.P) continue;
+        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+        float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) {
+            const float sc = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+            o[int64_t(co0 + j) * a.det_A] = sc;
+            const unsigned long long key =
+                (uint64_t(__float_as_uint(sc)) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(co0 + j));
+            bk[p] = key > bk[p] ? key : bk[p];
+          }
+      }
+    }
+    if (a.det_best) {
+#pragma unroll
+      for (int p = 0; p < RP; ++p) {
+        unsigned long long k = bk[p];
+        const unsigned long long k16 = __shfl_xor(k, 16);
+        k = k16 > k ? k16 : k;
+        const unsigned long long k32 = __shfl_xor(k, 32);
+        k = k32 > k ? k32 : k;
+        const int pix = pix_base + p * 16 + col;
+        if (grp == 0 && pix < a.P && k) {
+          const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+          atomicMax(a.det_best + int64_t(n) * a.det_A + a.det_a0 + q, k);
+        }
+      }
+    }
+    return;
+  }
+  float alpha = 1.f;
+  if (OUT == OUT_WSTORE || OUT == OUT_ACCUM) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+#pragma unroll
+  for (int r = 0; r < RC; ++r) {
+    const int co0 = (cot0 + r) * 16 + grp * 4;
+    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int pix = pix_base + p * 16 + col;
+      if (pix >= a.P) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(t) : t;
+      }
+      if (OUT == OUT_F32) {
+        float* yo = static_cast<float*>(a.y) + int64_t(pix) * a.ycs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          *reinterpret_cast<f4*>(yo) = f4{v[0], v[1], v[2], v[3]};
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) yo[j] = v[j];
+        }
+        continue;
+      }
+      _Float16* yo = static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co0;
+      if (a.res) {
+        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
+        }
+      }
+      if (OUT == OUT_WSTORE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha);
+      }
+      if (a.vec_ok && co0 + 3 < a.cout) {
+        if (OUT == OUT_ACCUM) {
+          h4 pv4 = *reinterpret_cast<const h4*>(yo);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin((float)pv4[j] + fpin(alpha * v[j]));
+        }
+        const h4 hv = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+        *reinterpret_cast<h4*>(yo) = hv;
+        if (OUT == OUT_F16 && a.dup && co0 >= a.duplo && co0 < a.duplo + a.dupn)  // dupn % 8 == 0 (host)
+          *reinterpret_cast<h4*>(a.dup + int64_t(pix) * a.dupcs + (co0 - a.duplo)) = hv;
+      } else {
+        for (int j = 0; j < 4; ++j) {
+          if (co0 + j >= a.cout) continue;
+          float t = v[j];
+          if (OUT == OUT_ACCUM) t = fpin((float)yo[j] + fpin(alpha * t));
+          yo[j] = (_Float16)fpin(t);
+          if (OUT == OUT_F16 && a.dup && co0 + j >= a.duplo && co0 + j < a.duplo + a.dupn)
+            a.dup[int64_t(pix) * a.dupcs + (co0 + j - a.duplo)] = (_Float16)fpin(t);
+        }
+      }
+    }
+  }
+}
+
+// NHWC source offset of output pixel `pix` of a 1x1 stride-1 conv (through the nearest x2^up upsampling)
+__device__ __forceinline__ int64_t conv1x1_src(const ConvArgs& a, int pix) {
+  if (!a.up) return int64_t(pix) * a.xcs;
+  const int hw = a.Ho * a.Wo;
+  const int n = pix / hw, r = pix - n * hw;
+  const int oy = r / a.Wo, ox = r - oy * a.Wo;
+  return nhwc_off(n, oy >> a.up, ox >> a.up, a.Hs, a.Ws, a.xcs);
+}
+
 // Big-tile LDS-DMA 3x3 configurations (conv3x3_big.hip), coded 0x800 | wm << 4 | (ab - 2) << 12: wm waves along
 // the couts, ab weight-stage buffers, 4 waves per block (8-wave blocks were measured and dropped);
 // stride 2 needs wm 2 (LDS)
@@ -124,5 +298,8 @@ int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hi
 // Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
 bool wide3_ok(int stride, int cw);
 int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
+// Big-tile 1x1 (conv1x1_big.hip), coded 0xB00 | log2(wc) << 4: 128 wc couts x 64 (8 / wc) pixels per 8-wave block
+bool big1_ok(int wc);
+int launch_big1(const ConvArgs& a, int out_kind, int wc, hipStream_t s);
 
 }  // namespace fce

@@ -582,8 +582,10 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (576, 256, 1, 1, 5, 7, False), (32, 32, 1, 1, 256, 256, False), (64, 48, 1, 1, 200, 200, True),
     (192, 128, 1, 1, 128, 160, False), (32, 64, 3, 2, 90, 100, False), (64, 48, 3, 1, 130, 70, True),
     (64, 80, 3, 2, 41, 37, False),
-    # wide 1x1s of the m/l scales (big-tile K-pipelined kernel, 0x7xx): odd K-step counts, partial cout tiles
+    # wide 1x1s of the m/l scales (big-tile K-pipelined kernel, 0x7xx; 256-wide tiles, 0xBxx): odd K-step counts,
+    # partial cout tiles / groups, partial pixel tiles, cin % 32 != 0
     (512, 256, 1, 1, 40, 40, True), (96, 256, 1, 1, 33, 35, False), (136, 72, 1, 1, 19, 23, True),
+    (200, 144, 1, 1, 17, 29, True), (1024, 512, 1, 1, 20, 20, False), (72, 384, 1, 1, 31, 9, False),
     # m/l 3x3s (A-in-LDS tile kernel, 0x81xx): partial cout groups, odd chunk counts, stride 2, residual
     (256, 256, 3, 1, 40, 40, True), (128, 80, 3, 2, 41, 37, False), (192, 128, 3, 1, 37, 29, True),
     (160, 48, 3, 1, 21, 19, False),
@@ -626,6 +628,7 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
     nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     assert any((codes[i] & 0xF00) == 0x400 for i in range(nv))
     assert any((codes[i] & 0xF00) == 0x700 for i in range(nv)) == (cin >= 64 and cout >= 64)
+    assert any((codes[i] & 0xF00) == 0xB00 for i in range(nv)) == (cin >= 64 and cout >= 128)
     outs = {}
     for code in [-1] + list(codes[:nv]):
         y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
