@@ -16,6 +16,70 @@
 
 namespace fce {
 
+// Staged fp16 output (OUT_F16 / OUT_WSTORE with a.stg): the block's BP x BC*16 output tile is assembled in LDS
+// (pixel rows of BC*16 halves, 16-byte slot sl of pixel px at sl ^ (px & (NSL - 1))) and written with 16-byte lane
+// stores, whole pixel rows per NSL lanes.  The fragment-layout stores (8 bytes per lane, 16 pixels x 32 bytes per
+// instruction) were the bound of this kernel: 512 -> 512 at 80^2, bs 32 ran 275 us with them and 132 us without
+// any store (FCE_BIG1_DIAG=1).  Values exactly as conv_epilogue / conv_store_staged: bitwise the same.
+template <int BC, int BP, int OUT>
+__device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8][4], int p0, int wc, int wp, int cbl0,
+                                                  int col, int grp, _Float16* ot) {
+  constexpr int ROW = BC * 16, NSL = 2 * BC;
+  const int cotiles = (a.cout + 15) >> 4;
+  float alpha = 1.f;
+  if (OUT == OUT_WSTORE) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int ctl = wc * 8 + r;
+    const int co0 = (cbl0 + ctl) * 16 + grp * 4;
+    if (cbl0 + ctl >= cotiles) continue;
+    float bz[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int px = wp * 64 + p * 16 + col, pix = p0 + px;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = acc[r][p][j] + bz[j];
+        v[j] = a.act ? silu(t) : t;
+      }
+      if (a.res && pix < a.P) {
+        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
+        if (a.vec_ok && co0 + 3 < a.cout) {
+          const h4 rv = *reinterpret_cast<const h4*>(ro);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
+        }
+      }
+      if (OUT == OUT_WSTORE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha);
+      }
+      const int sl = ctl * 2 + (grp >> 1);
+      *reinterpret_cast<h4*>(ot + px * ROW + ((sl ^ (px & (NSL - 1))) * 8) + (grp & 1) * 4) =
+          h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+    }
+  }
+  __syncthreads();
+  constexpr int NP = BP * NSL;  // 16-byte pieces of the tile (a multiple of 512)
+#pragma unroll 4
+  for (int e = int(threadIdx.x); e < NP; e += 512) {
+    const int px = e / NSL, sl = e - px * NSL;
+    const int pix = p0 + px, co = cbl0 * 16 + sl * 8;
+    if (pix < a.P && co < a.cout) {
+      const h8 hv = *reinterpret_cast<const h8*>(ot + px * ROW + (sl ^ (px & (NSL - 1))) * 8);
+      *reinterpret_cast<h8*>(static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co) = hv;
+      if (OUT == OUT_F16 && a.dup && co >= a.duplo && co < a.duplo + a.dupn)
+        *reinterpret_cast<h8*>(a.dup + int64_t(pix) * a.dupcs + (co - a.duplo)) = hv;
+    }
+  }
+}
+
 template <int WC>
 struct Big1Geom {
   static constexpr int WP = 8 / WC;
@@ -35,7 +99,9 @@ __device__ __forceinline__ void b1_glds16(const void* src, h8* lds_wave_base) {
                                    (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
 }
 
-template <int WC, int OUT>
+// DIAG (diagnostics only, FCE_BIG1_DIAG): 1 = no output stores (a guard that never fires keeps the MFMAs live),
+// 2 = no copies after the prologue (MFMAs on stale slots), 3 = no MFMAs (copies + fragment reads only)
+template <int WC, int OUT, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void conv1x1_big_kernel(ConvArgs a) {
   using G = Big1Geom<WC>;
   constexpr int WP = G::WP, BC = G::BC, BP = G::BP, NA = G::NA, NB = G::NB, IA = G::IA, IB = G::IB, RING = G::RING;
@@ -96,7 +162,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_big_kernel(ConvArgs a) {
     // this wave's copies of step s have landed once only the (RING - 2) later steps' remain outstanding
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (IA + IB)) : "memory");
     __syncthreads();  // every wave's copies of step s visible; step s - 1's reads done (slot (s - 1) % RING free)
-    issue(s + RING - 1);
+    if (DIAG != 2) issue(s + RING - 1);
     const h8* cur = big1_smem + (s % RING) * (NA + NB);
     const h8* As = cur + (wc * 8) * 64 + lane;
     const h8* Bs = cur + NA;
@@ -106,25 +172,59 @@ __global__ __launch_bounds__(512, 1) void conv1x1_big_kernel(ConvArgs a) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const h8 af = As[r * 64];
+      if (DIAG == 3) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[r][p][0] += (float)af[p] + (float)bf[p][r];
+        continue;
+      }
 #pragma unroll
       for (int p = 0; p < 4; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[p], acc[r][p], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no copy may land after the block exits
+  if (DIAG == 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) t += acc[r][p][0] + acc[r][p][1] + acc[r][p][2] + acc[r][p][3];
+    if (t == 1234.5678f) static_cast<_Float16*>(a.y)[tid] = (_Float16)t;
+    return;
+  }
+  if constexpr (OUT == OUT_F16 || OUT == OUT_WSTORE) {
+    if (a.stg) {  // the ring is free once every wave is past its last step (BP x BC*16 halves fit in it)
+      static_assert(size_t(BP) * BC * 16 * 2 <= G::lds, "staged output tile exceeds the ring");
+      __syncthreads();
+      big1_store_staged<BC, BP, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
+      return;
+    }
+  }
   conv_epilogue<8, 4, OUT>(a, acc, p0 + wp * 64, ct_blk + wc * 8, col, grp);
 }
 
 bool big1_ok(int wc) { return wc == 1 || wc == 2; }
 
-template <int WC, int OUT>
-static int launch_big1_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
+template <int WC, int OUT, int DIAG>
+static int launch_big1_d(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr size_t lds = Big1Geom<WC>::lds;
   static_assert(lds <= 160 * 1024, "big 1x1 tile: LDS over 160 KiB");
-  static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_big_kernel<WC, OUT>),
+  static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_big_kernel<WC, OUT, DIAG>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!big) return fail(FCE_ERR_HIP, "conv 1x1 big tile: cannot opt in to >64 KiB LDS");
-  FCE_LAUNCH((conv1x1_big_kernel<WC, OUT>), grid, dim3(512), lds, s, a);
+  FCE_LAUNCH((conv1x1_big_kernel<WC, OUT, DIAG>), grid, dim3(512), lds, s, a);
   return FCE_OK;
+}
+
+template <int WC, int OUT>
+static int launch_big1_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
+  static const int diag = [] {
+    const char* e = getenv("FCE_BIG1_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  if (OUT == OUT_F16 && diag == 1) return launch_big1_d<WC, OUT, 1>(a, grid, s);
+  if (OUT == OUT_F16 && diag == 2) return launch_big1_d<WC, OUT, 2>(a, grid, s);
+  if (OUT == OUT_F16 && diag == 3) return launch_big1_d<WC, OUT, 3>(a, grid, s);
+  return launch_big1_d<WC, OUT, 0>(a, grid, s);
 }
 
 template <int WC>
