@@ -120,7 +120,7 @@ struct ConvDepth {
   static constexpr int D = RC * RP == 1 ? 8 : RC * RP == 2 ? 4 : 2;
 };
 
-// conv_epilogue (the dense MFMA kernels' epilogue) lives in conv_args.h, shared with conv1x1_big.hip
+// conv_epilogue (the dense MFMA kernels' epilogue) lives in conv_args.h, shared with conv_big.hip
 
 template <int KS, int RC, int RP, int OUT, bool FAST>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
@@ -2213,6 +2213,11 @@ static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (rin
   return v;
 }
 
+static bool no_gemm3() {  // diagnostics / A-B runs: FCE_NO_GEMM3=1 drops the implicit-GEMM 3x3 candidates (0xC00)
+  const char* e = getenv("FCE_NO_GEMM3");
+  return e && atoi(e) != 0;
+}
+
 static bool wide3_on() {  // read per call, like FCE_TILE3AL (the variant tests switch it on mid-process)
   const char* e = getenv("FCE_WIDE3");
   return e && atoi(e) != 0;
@@ -2291,6 +2296,9 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int ab : {2, 3})
       for (int wm : {1, 2})
         if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 128 && !det_box && !no_gemm3())  // 0xC00
+    for (int wcl = 0; wcl < 2; ++wcl)
+      if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xC00 | (wcl << 4);
   // wide tile (opt-in, FCE_WIDE3=1: measured at parity or slower on every m/l shape): 0xA00 | cwl << 4
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && wide3_on())
     for (int cwl = 0; cwl < 3; ++cwl)
@@ -2724,6 +2732,12 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0xEF) == 0 && out_kind != OUT_DFL && big1_ok(wc),
               "conv: bad big-tile 1x1 hint");
     return launch_big1(a, out_kind, wc, s);
+  }
+  if (kind == 12) {  // 256-wide-tile implicit-GEMM 3x3 kernel
+    const int wc = 1 << ((tile >> 4) & 1);
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xEF) == 0 && big1_ok(wc),
+              "conv: bad big-tile 3x3 (implicit GEMM) hint");
+    return launch_big3g(a, wc, d.stride, s);
   }
   if (kind == 10) {  // wide-tile 3x3 kernel, per-K-step weight staging
     const int cw = 1 << ((tile >> 4) & 3);

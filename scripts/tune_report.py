@@ -28,7 +28,9 @@ ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--imgsz", type=int, default=640)
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-model = DetectionModel(a.model)
+from bench import model_cfg  # noqa: E402  (the "-h8" BASELINE config)
+
+model = DetectionModel(model_cfg(a.model))
 model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
 model.eval().to(dev)
 eng = Engine(model, a.batch, a.imgsz, dev)

@@ -594,6 +594,8 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (160, 48, 3, 1, 21, 19, False),
     # big-tile LDS-DMA 3x3 (0x8x0): stride 2 with partial cout groups / edge tiles, residual
     (128, 136, 3, 2, 41, 37, False), (96, 192, 3, 2, 33, 47, True), (64, 96, 3, 1, 19, 35, True),
+    # 256-wide implicit-GEMM 3x3 (0xCx0): stride 2 over odd maps with partial pixel tiles, residual, 512 couts
+    (512, 256, 3, 2, 21, 19, True), (64, 512, 3, 1, 13, 11, False),
 ]
 
 
