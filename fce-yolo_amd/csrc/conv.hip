@@ -2262,9 +2262,10 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
           if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
           if (n < cap) out[n++] = 0x500 | rc | (rp << 4) | (wl << 12);
         }
-  if (d.k == 1 && d.stride == 1 && !det_box && d.cin >= 64 && d.cout >= 128)  // 256-wide tiles: 0xB00 | log2(wc) << 4
-    for (int wcl = 0; wcl < 2; ++wcl)
-      if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xB00 | (wcl << 4);
+  if (d.k == 1 && d.stride == 1 && !det_box && d.cin >= 64 && d.cout >= 128)  // big tiles: 0xB00 | log2(wc) << 4 | nw4
+    for (int nw4 : {0, 1})
+      for (int wcl = 0; wcl < 2; ++wcl)
+        if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xB00 | (wcl << 4) | (nw4 << 6);
   if (pipe1_ok(d, det_box))  // big-tile K-pipelined 1x1: 0x700 | log2(wp) << 12
     for (int wl = 0; wl < 3; ++wl) {
       const int cb = (4 >> wl) * 4;
@@ -2297,8 +2298,9 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int wm : {1, 2})
         if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 128 && !det_box && !no_gemm3())  // 0xC00
-    for (int wcl = 0; wcl < 2; ++wcl)
-      if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xC00 | (wcl << 4);
+    for (int nw4 : {0, 1})
+      for (int wcl = 0; wcl < 2; ++wcl)
+        if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xC00 | (wcl << 4) | (nw4 << 6);
   // wide tile (opt-in, FCE_WIDE3=1: measured at parity or slower on every m/l shape): 0xA00 | cwl << 4
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && wide3_on())
     for (int cwl = 0; cwl < 3; ++cwl)
@@ -2728,16 +2730,16 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     return launch_big3(a, wm, ab, nw, d.stride, x.n, s);
   }
   if (kind == 11) {  // 256-wide-tile 1x1 kernel
-    const int wc = 1 << ((tile >> 4) & 1);
-    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0xEF) == 0 && out_kind != OUT_DFL && big1_ok(wc),
+    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8;
+    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0xAF) == 0 && out_kind != OUT_DFL && big1_ok(wc),
               "conv: bad big-tile 1x1 hint");
-    return launch_big1(a, out_kind, wc, s);
+    return launch_big1(a, out_kind, wc, nw, s);
   }
   if (kind == 12) {  // 256-wide-tile implicit-GEMM 3x3 kernel
-    const int wc = 1 << ((tile >> 4) & 1);
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xEF) == 0 && big1_ok(wc),
+    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xAF) == 0 && big1_ok(wc),
               "conv: bad big-tile 3x3 (implicit GEMM) hint");
-    return launch_big3g(a, wc, d.stride, s);
+    return launch_big3g(a, wc, nw, d.stride, s);
   }
   if (kind == 10) {  // wide-tile 3x3 kernel, per-K-step weight staging
     const int cw = 1 << ((tile >> 4) & 3);

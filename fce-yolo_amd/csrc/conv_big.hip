@@ -30,7 +30,7 @@ namespace fce {
 // stores, whole pixel rows per NSL lanes.  The fragment-layout stores (8 bytes per lane, 16 pixels x 32 bytes per
 // instruction) were the bound of this kernel: 512 -> 512 at 80^2, bs 32 ran 275 us with them and 132 us without
 // any store (FCE_BIG1_DIAG=1).  Values exactly as conv_epilogue / conv_store_staged: bitwise the same.
-template <int BC, int BP, int OUT>
+template <int BC, int BP, int NT, int OUT>
 __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8][4], int p0, int wc, int wp, int cbl0,
                                                   int col, int grp, _Float16* ot) {
   constexpr int ROW = BC * 16, NSL = 2 * BC;
@@ -75,9 +75,10 @@ __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8
     }
   }
   __syncthreads();
-  constexpr int NP = BP * NSL;  // 16-byte pieces of the tile (a multiple of 512)
+  constexpr int NP = BP * NSL;  // 16-byte pieces of the tile (a multiple of NT)
+  static_assert(NP % NT == 0, "whole store rounds");
 #pragma unroll 4
-  for (int e = int(threadIdx.x); e < NP; e += 512) {
+  for (int e = int(threadIdx.x); e < NP; e += NT) {
     const int px = e / NSL, sl = e - px * NSL;
     const int pix = p0 + px, co = cbl0 * 16 + sl * 8;
     if (pix < a.P && co < a.cout) {
@@ -89,20 +90,23 @@ __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8
   }
 }
 
-template <int WC, int RING_ = 4>
+template <int WC, int NW, int RING_>
 struct Big1Geom {
-  static constexpr int WP = 8 / WC;
+  static constexpr int WP = NW / WC;
   static constexpr int BC = WC * 8;     // cout tiles per block
   static constexpr int BP = WP * 64;    // pixels per block
   static constexpr int NA = BC * 64;    // A pieces (16 B) per K-step = BC DMA instructions (1 KiB each)
   static constexpr int NB = BP * 4;     // B pieces per K-step = NB / 64 DMA instructions
-  static constexpr int IA = BC / 8, IB = NB / 64 / 8;  // DMA instructions per wave per K-step
+  static constexpr int IA = BC / NW, IB = NB / 64 / NW;  // DMA instructions per wave per K-step
   static constexpr int RING = RING_;    // K-step slots: the copies of step s + RING - 1 go out while step s computes
   static constexpr size_t lds = size_t(RING) * (NA + NB) * 16;
+  static_assert(BC % NW == 0 && (NB / 64) % NW == 0, "whole DMA rounds per wave");
 };
 
-// ring slots: 5 when a slot is 32 KiB (WC = 2), 4 for the 40 KiB slots of WC = 1 (copies issued 4 / 3 steps ahead)
-constexpr int big_ring(int wc) { return wc == 2 ? 5 : 4; }
+// ring slots.  8-wave blocks (one per CU): 5 when a slot is 32 KiB (WC = 2), 4 for the 40 KiB slots of WC = 1
+// (copies issued 4 / 3 steps ahead).  4-wave blocks (two per CU, 24 KiB slots): 3, so two blocks fit in the LDS and
+// one block's prologue / staged epilogue overlaps the other's K loop
+constexpr int big_ring(int wc, int nw) { return nw == 4 ? 3 : wc == 2 ? 5 : 4; }
 
 __device__ __forceinline__ int b1_slot(int u, int q) { return u * 4 + (q ^ ((u >> 1) & 3)); }
 
@@ -116,10 +120,11 @@ __device__ __forceinline__ void b1_glds16(const void* src, h8* lds_wave_base) {
 // K loop: the next step's fragments are read into a second register set while this step's MFMAs run, so the copies
 // are waited for one step ahead of their use (4.5-8 % over reading them after the step's barrier, l/m shapes on one
 // box; s_setprio 1 around the MFMAs measured slower)
-template <int KS, int S, int WC, int OUT, int DIAG = 0>
-__global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
+template <int KS, int S, int WC, int NW, int OUT, int DIAG = 0>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(ConvArgs a) {
   static_assert(KS == 1 ? S == 1 : (KS == 3 && (S == 1 || S == 2)), "conv big tile: 1x1 s1 or 3x3 s1 / s2");
-  using G = Big1Geom<WC, big_ring(WC)>;
+  static_assert(NW == 8 || NW == 4, "conv big tile: 8- or 4-wave blocks");
+  using G = Big1Geom<WC, NW, big_ring(WC, NW)>;
   constexpr int WP = G::WP, BC = G::BC, BP = G::BP, NA = G::NA, NB = G::NB, IA = G::IA, IB = G::IB, RING = G::RING;
   extern __shared__ __attribute__((aligned(16))) h8 big1_smem[];  // RING x [A | B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
   const h8* asrc[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
-    const int ct = min(ct_blk + wave + 8 * j, cotiles - 1);
+    const int ct = min(ct_blk + wave + NW * j, cotiles - 1);
     asrc[j] = wts + size_t(ct) * a.nalloc * 64 + lane;
   }
   // B sources.  1x1: the pixel's piece (through the x2^up upsampling), -1 past P.  3x3: the piece of input pixel
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
   unsigned bm[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) {
-    const int e = (wave + 8 * j) * 64 + lane;
+    const int e = (wave + NW * j) * 64 + lane;
     const int u = e >> 2, q = (e & 3) ^ ((u >> 1) & 3), pix = p0 + u;
     bq[j] = q * 8;
     if constexpr (KS == 1) {
@@ -182,13 +187,13 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
   auto issue = [&](int t) {  // step t's copies into ring slot t % RING
     h8* slot = big1_smem + (t % RING) * (NA + NB);
 #pragma unroll
-    for (int j = 0; j < IA; ++j) b1_glds16(asrc[j] + size_t(t) * 64, slot + (wave + 8 * j) * 64);  // zero steps past nst
+    for (int j = 0; j < IA; ++j) b1_glds16(asrc[j] + size_t(t) * 64, slot + (wave + NW * j) * 64);  // zero steps past nst
     if constexpr (KS == 1) {
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
         const bool ok = boff[j] >= 0 && t * 32 + bq[j] < a.cin;
         b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + t * 32) : zl,
-                  slot + NA + (wave + 8 * j) * 64);
+                  slot + NA + (wave + NW * j) * 64);
       }
     } else {
       const int64_t toff = int64_t(iky * a.Ws + ikx) * a.xcs + ic * 32;
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
       for (int j = 0; j < IB; ++j) {
         const bool ok = live && (bm[j] & need) == need;
         b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + toff) : zl,
-                  slot + NA + (wave + 8 * j) * 64);
+                  slot + NA + (wave + NW * j) * 64);
       }
       if (++ikx == 3) {
         ikx = 0;
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
     if (a.stg) {  // the ring is free once every wave is past its last step (BP x BC*16 halves fit in it)
       static_assert(size_t(BP) * BC * 16 * 2 <= G::lds, "staged output tile exceeds the ring");
       __syncthreads();
-      big1_store_staged<BC, BP, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
+      big1_store_staged<BC, BP, NW * 64, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
       return;
     }
   }
@@ -281,74 +286,84 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(ConvArgs a) {
 
 bool big1_ok(int wc) { return wc == 1 || wc == 2; }
 
-template <int KS, int S, int WC, int OUT, int DIAG>
+template <int KS, int S, int WC, int NW, int OUT, int DIAG>
 static int launch_big_d(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr size_t lds = Big1Geom<WC, big_ring(WC)>::lds;
-  static_assert(lds <= 160 * 1024, "big tile: LDS over 160 KiB");
+  constexpr size_t lds = Big1Geom<WC, NW, big_ring(WC, NW)>::lds;
+  static_assert(lds * (NW == 4 ? 2 : 1) <= 160 * 1024, "big tile: LDS over 160 KiB per CU");
   static const bool big =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, OUT, DIAG>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, NW, OUT, DIAG>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!big) return fail(FCE_ERR_HIP, "conv big tile: cannot opt in to >64 KiB LDS");
-  FCE_LAUNCH((conv_big_kernel<KS, S, WC, OUT, DIAG>), grid, dim3(512), lds, s, a);
+  FCE_LAUNCH((conv_big_kernel<KS, S, WC, NW, OUT, DIAG>), grid, dim3(NW * 64), lds, s, a);
   return FCE_OK;
 }
 
-template <int KS, int S, int WC, int OUT>
+template <int KS, int S, int WC, int NW, int OUT>
 static int launch_big_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
   static const int diag = [] {
     const char* e = getenv("FCE_BIG1_DIAG");
     return e ? atoi(e) : 0;
   }();
   if constexpr (OUT == OUT_F16) {
-    if (diag == 1) return launch_big_d<KS, S, WC, OUT, 1>(a, grid, s);
-    if (diag == 2) return launch_big_d<KS, S, WC, OUT, 2>(a, grid, s);
-    if (diag == 3) return launch_big_d<KS, S, WC, OUT, 3>(a, grid, s);
+    if (diag == 1) return launch_big_d<KS, S, WC, NW, OUT, 1>(a, grid, s);
+    if (diag == 2) return launch_big_d<KS, S, WC, NW, OUT, 2>(a, grid, s);
+    if (diag == 3) return launch_big_d<KS, S, WC, NW, OUT, 3>(a, grid, s);
   }
-  return launch_big_d<KS, S, WC, OUT, 0>(a, grid, s);
+  return launch_big_d<KS, S, WC, NW, OUT, 0>(a, grid, s);
 }
 
-template <int WC>
+template <int WC, int NW>
 static int launch_big1_w(const ConvArgs& a, int out_kind, dim3 grid, hipStream_t s) {
   switch (out_kind) {
-    case OUT_F16: return launch_big_k<1, 1, WC, OUT_F16>(a, grid, s);
-    case OUT_F32: return launch_big_k<1, 1, WC, OUT_F32>(a, grid, s);
-    case OUT_WSTORE: return launch_big_k<1, 1, WC, OUT_WSTORE>(a, grid, s);
-    case OUT_ACCUM: return launch_big_k<1, 1, WC, OUT_ACCUM>(a, grid, s);
-    case OUT_CLS: return launch_big_k<1, 1, WC, OUT_CLS>(a, grid, s);
+    case OUT_F16: return launch_big_k<1, 1, WC, NW, OUT_F16>(a, grid, s);
+    case OUT_F32: return launch_big_k<1, 1, WC, NW, OUT_F32>(a, grid, s);
+    case OUT_WSTORE: return launch_big_k<1, 1, WC, NW, OUT_WSTORE>(a, grid, s);
+    case OUT_ACCUM: return launch_big_k<1, 1, WC, NW, OUT_ACCUM>(a, grid, s);
+    case OUT_CLS: return launch_big_k<1, 1, WC, NW, OUT_CLS>(a, grid, s);
     default: return fail(FCE_ERR_INVALID, "conv 1x1 big tile: unsupported epilogue");
   }
 }
 
-static ConvArgs big_grid(const ConvArgs& a0, int wc, dim3& grid) {
+static ConvArgs big_grid(const ConvArgs& a0, int wc, int nw, dim3& grid) {
   ConvArgs a = a0;
-  const int bp = (8 / wc) * 64, bc = wc * 8;
+  const int bp = (nw / wc) * 64, bc = wc * 8;
   a.gy = ((a.cout + 15) / 16 + bc - 1) / bc;
   const int64_t tiles = (int64_t(a.P) + bp - 1) / bp;
   grid = dim3(unsigned(std::min<int64_t>(tiles * a.gy, int64_t(1) << 31)));
   return a;
 }
 
-int launch_big1(const ConvArgs& a0, int out_kind, int wc, hipStream_t s) {
-  FCE_CHECK(big1_ok(wc) && a0.cin % 8 == 0 && out_kind != OUT_DFL, "conv 1x1 big tile: bad configuration");
+int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, hipStream_t s) {
+  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && a0.cin % 8 == 0 && out_kind != OUT_DFL,
+            "conv 1x1 big tile: bad configuration");
   dim3 grid;
-  const ConvArgs a = big_grid(a0, wc, grid);
+  const ConvArgs a = big_grid(a0, wc, nw, grid);
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 1x1 big tile: grid too large");
-  const int rc = wc == 1 ? launch_big1_w<1>(a, out_kind, grid, s) : launch_big1_w<2>(a, out_kind, grid, s);
+  int rc;
+  if (nw == 8)
+    rc = wc == 1 ? launch_big1_w<1, 8>(a, out_kind, grid, s) : launch_big1_w<2, 8>(a, out_kind, grid, s);
+  else
+    rc = wc == 1 ? launch_big1_w<1, 4>(a, out_kind, grid, s) : launch_big1_w<2, 4>(a, out_kind, grid, s);
   if (rc != FCE_OK) return rc;
   return launch_status("conv_big_kernel");
 }
 
-int launch_big3g(const ConvArgs& a0, int wc, int stride, hipStream_t s) {
-  FCE_CHECK(big1_ok(wc) && a0.cin % 32 == 0 && a0.up == 0 && (stride == 1 || stride == 2),
+template <int S, int NW>
+static int launch_big3g_s(const ConvArgs& a, int wc, dim3 grid, hipStream_t s) {
+  return wc == 1 ? launch_big_k<3, S, 1, NW, OUT_F16>(a, grid, s) : launch_big_k<3, S, 2, NW, OUT_F16>(a, grid, s);
+}
+
+int launch_big3g(const ConvArgs& a0, int wc, int nw, int stride, hipStream_t s) {
+  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && a0.cin % 32 == 0 && a0.up == 0 && (stride == 1 || stride == 2),
             "conv 3x3 big tile: bad configuration");
   dim3 grid;
-  const ConvArgs a = big_grid(a0, wc, grid);
+  const ConvArgs a = big_grid(a0, wc, nw, grid);
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 3x3 big tile: grid too large");
   int rc;
   if (stride == 1)
-    rc = wc == 1 ? launch_big_k<3, 1, 1, OUT_F16>(a, grid, s) : launch_big_k<3, 1, 2, OUT_F16>(a, grid, s);
+    rc = nw == 8 ? launch_big3g_s<1, 8>(a, wc, grid, s) : launch_big3g_s<1, 4>(a, wc, grid, s);
   else
-    rc = wc == 1 ? launch_big_k<3, 2, 1, OUT_F16>(a, grid, s) : launch_big_k<3, 2, 2, OUT_F16>(a, grid, s);
+    rc = nw == 8 ? launch_big3g_s<2, 8>(a, wc, grid, s) : launch_big3g_s<2, 4>(a, wc, grid, s);
   if (rc != FCE_OK) return rc;
   return launch_status("conv_big_kernel");
 }

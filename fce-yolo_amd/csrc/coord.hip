@@ -26,12 +26,20 @@ enum { ACT_NONE_ = 0, ACT_SILU_ = 1, ACT_SIGMOID_ = 2 };
 struct CoordWs {
   float* xh;      // N*H*C
   float* xw;      // N*W*C
+  float* part;    // N*bands*W*C: column sums of each row band (band pooling)
   float* buf[6];  // N*L*mid each
   float* g1;      // N*H*oup
   float* g2;      // N*W*oup
 };
 
 static size_t align_f(size_t n) { return (n + 63) & ~size_t(63); }
+
+// Band pooling (one read of x) for C >= 256 (C % 64 == 0, W <= 256); rows per band so that the grid has >= 512
+// blocks when it can.  At C = 128 (n scale) the two-pass kernel stays: its extra read hits L2 and the band path's
+// second launch costs more (n L5 58.5 vs 62.0 us per call; l L5 256 -> 252, m L5 434.5 -> 422.6, r03r)
+static constexpr int kBandMaxK = 8;  // columns per thread: W <= 32 * kBandMaxK
+static bool band_pool_ok(int C, int W) { return C >= 256 && C % 64 == 0 && W <= 32 * kBandMaxK; }
+static int band_rows(int N, int H, int C) { return int64_t(N) * ((H + 15) / 16) * (C / 64) >= 512 ? 16 : 8; }
 
 static size_t ws_layout(const fce_coord_desc& d, int n, int h, int w, CoordWs* out, float* base) {
   const int L = h > w ? h : w;
@@ -45,6 +53,8 @@ static size_t ws_layout(const fce_coord_desc& d, int n, int h, int w, CoordWs* o
   CoordWs ws;
   ws.xh = take(size_t(n) * h * d.inp);
   ws.xw = take(size_t(n) * w * d.inp);
+  const int R = band_rows(n, h, d.inp);
+  ws.part = band_pool_ok(d.inp, w) ? take(size_t(n) * ((h + R - 1) / R) * w * d.inp) : nullptr;
   for (int i = 0; i < 6; ++i) ws.buf[i] = take(size_t(n) * L * mx);
   ws.g1 = take(size_t(n) * h * d.oup);
   ws.g2 = take(size_t(n) * w * d.oup);
@@ -160,6 +170,93 @@ __global__ __launch_bounds__(256) void pool_kernel(const _Float16* x, int xcs, i
     pool_rows(x, xcs, H, W, C, xh, j, n);
   else
     pool_cols(x, xcs, H, W, C, xw, j - H, n);
+}
+
+// Band pooling: x is read ONCE.  Block (image n, band of R rows, 64-channel slice): thread (cg = t & 7, xt = t >> 3)
+// loads the 8 channels cg of its columns xx = xt + 32 k of every band row; per row it adds them into its column
+// sums (registers) and its row sum, the 32 row sums of a channel group are added by an xor tree over the 8 lanes of
+// the wave that share cg and then over the 4 waves in order (LDS), so the row means come out complete; the column
+// sums of the band go to part[n][band][x][c] and pool_band_cols_kernel adds the bands in order.  Fixed orders
+// throughout: deterministic.  (The two-pass pool_kernel above re-reads x for the columns: 1.19-1.45x the
+// algorithmic bytes in PMC.)
+template <int R, int KW>
+__global__ __launch_bounds__(256) void pool_band_kernel(const _Float16* x, int xcs, int H, int W, int C, float* xh,
+                                                        float* part, int NB) {
+  __shared__ float red[R][4][64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int cg = t & 7, xt = t >> 3;
+  const int ncs = C >> 6;
+  int b = int(blockIdx.x);
+  const int cs = b % ncs;
+  b /= ncs;
+  const int band = b % NB, n = b / NB;
+  const int y0 = band * R, y1 = min(H, y0 + R);
+  const int c0 = cs * 64 + cg * 8;
+  const _Float16* xn = x + nhwc_off(n, 0, 0, H, W, xcs) + c0;
+  float col[KW][8];
+#pragma unroll
+  for (int k = 0; k < KW; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) col[k][j] = 0.f;
+  for (int y = y0; y < y1; ++y) {
+    h8 v[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int xx = xt + 32 * k;
+      v[k] = xx < W ? *reinterpret_cast<const h8*>(xn + (int64_t(y) * W + xx) * xcs) : h8{};
+    }
+    float r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (float)v[k][j];
+        col[k][j] += f;
+        r[j] += f;
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r[j] += __shfl_xor(r[j], 8);
+      r[j] += __shfl_xor(r[j], 16);
+      r[j] += __shfl_xor(r[j], 32);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[y - y0][wave][cg * 8 + j] = r[j];
+    }
+  }
+  __syncthreads();
+  const float inv = 1.0f / (float)W;
+  for (int e = t; e < (y1 - y0) * 64; e += 256) {
+    const int yy = e >> 6, c = e & 63;
+    const float sum = ((red[yy][0][c] + red[yy][1][c]) + red[yy][2][c]) + red[yy][3][c];
+    xh[(int64_t(n) * H + y0 + yy) * C + cs * 64 + c] = sum * inv;
+  }
+  float* pb = part + (int64_t(n) * NB + band) * W * C + c0;
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    const int xx = xt + 32 * k;
+    if (xx < W) {
+      float* o = pb + int64_t(xx) * C;
+      *reinterpret_cast<f4*>(o) = f4{col[k][0], col[k][1], col[k][2], col[k][3]};
+      *reinterpret_cast<f4*>(o + 4) = f4{col[k][4], col[k][5], col[k][6], col[k][7]};
+    }
+  }
+}
+
+// xw[n][x][c] = (sum over bands, in order, of part[n][band][x][c]) / H; 4 channels per thread
+__global__ __launch_bounds__(256) void pool_band_cols_kernel(const float* part, float* xw, int N, int NB, int H, int WC) {
+  const int64_t e = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (e >= int64_t(N) * WC) return;
+  const int64_t n = e / WC, r = e - n * WC;
+  const float* p = part + n * NB * WC + r;
+  f4 s = *reinterpret_cast<const f4*>(p);
+  for (int b = 1; b < NB; ++b) {
+    const f4 v = *reinterpret_cast<const f4*>(p + int64_t(b) * WC);
+    s = f4{s[0] + v[0], s[1] + v[1], s[2] + v[2], s[3] + v[3]};
+  }
+  const float inv = 1.0f / (float)H;
+  *reinterpret_cast<f4*>(xw + e) = f4{s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv};
 }
 
 // ---------------------------------------------------------------------------- 2. projections
@@ -779,14 +876,19 @@ template <int MODE, int GPX>
 __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int xcs, _Float16* y, int ycs, int N,
                                                          int H, int W, int C, const float* g1, const float* g2) {
   const int CG = C / 8;
-  const int row = blockIdx.y, n = row / H, yy = row - n * H;
+  // 1-D grid, XCD-aware: block b runs on XCD b % 8 and takes logical block (b % 8) * per + b / 8, so each XCD walks
+  // a contiguous range of rows (whole images): an image's column gates g2 (W x C fp32) enter one L2, not eight
+  const int gx = (W * CG + 256 * GPX - 1) / (256 * GPX);
+  const int total = int(gridDim.x), b = int(blockIdx.x), per = total >> 3, body = per << 3;
+  const int L = b < body ? (b & 7) * per + (b >> 3) : b;
+  const int row = L / gx, bx = L - row * gx, n = row / H, yy = row - n * H;
   h8 v[GPX];
   f4 ga[GPX][2], gb[GPX][2];
   int xx[GPX], gg[GPX];
   bool live[GPX];
 #pragma unroll
   for (int k = 0; k < GPX; ++k) {
-    const int e = (blockIdx.x * GPX + k) * 256 + threadIdx.x;
+    const int e = (bx * GPX + k) * 256 + threadIdx.x;
     live[k] = e < W * CG;
     const int ec = live[k] ? e : 0;
     xx[k] = ec / CG;
@@ -1026,14 +1128,32 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
   ws_layout(d, N, H, W, &w, static_cast<float*>(ws));
   const _Float16* xp = static_cast<const _Float16*>(x.data) + x.coff;
   const int C = d.inp, mid = d.mid;
-  int RG = 1;  // pool_col_groups on the host
-  while (RG < 8 && (C / 8) * RG * 2 <= 256 && H >= 16 * RG) RG *= 2;
-  const int XW = 256 / ((C / 8) * RG);
-  const int BPI = H + (W + XW - 1) / XW;
-  const int aff = N >= 8;
-  const int64_t nblk = int64_t(aff ? 8 * ((N + 7) / 8) : N) * BPI;
-  FCE_CHECK(nblk < (int64_t(1) << 31), "coord pooling: grid too large");
-  FCE_LAUNCH(pool_kernel, dim3(unsigned(nblk)), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.xw, N, BPI, aff);
+  const char* tp = getenv("FCE_COORD_TWO_PASS");  // diagnostics: the two-pass row / column pooling
+  if (w.part && !(tp && atoi(tp))) {  // band pooling: one read of x
+    const int R = band_rows(N, H, C), NB = (H + R - 1) / R;
+    const int64_t nblk = int64_t(N) * NB * (C / 64);
+    FCE_CHECK(nblk < (int64_t(1) << 31), "coord pooling: grid too large");
+#define FCE_BAND(RR, KK) \
+  FCE_LAUNCH((pool_band_kernel<RR, KK>), dim3(unsigned(nblk)), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.part, NB)
+    const int kw = (W + 31) / 32;  // columns per thread: 3 (W <= 96), 5 (<= 160) or 8 registers' worth
+    if (R == 16) {
+      if (kw <= 3) FCE_BAND(16, 3); else if (kw <= 5) FCE_BAND(16, 5); else FCE_BAND(16, 8);
+    } else {
+      if (kw <= 3) FCE_BAND(8, 3); else if (kw <= 5) FCE_BAND(8, 5); else FCE_BAND(8, 8);
+    }
+#undef FCE_BAND
+    const int64_t ncol = (int64_t(N) * W * C / 4 + 255) / 256;
+    FCE_LAUNCH(pool_band_cols_kernel, dim3(unsigned(ncol)), dim3(256), 0, s, w.part, w.xw, N, NB, H, W * C);
+  } else {
+    int RG = 1;  // pool_col_groups on the host
+    while (RG < 8 && (C / 8) * RG * 2 <= 256 && H >= 16 * RG) RG *= 2;
+    const int XW = 256 / ((C / 8) * RG);
+    const int BPI = H + (W + XW - 1) / XW;
+    const int aff = N >= 8;
+    const int64_t nblk = int64_t(aff ? 8 * ((N + 7) / 8) : N) * BPI;
+    FCE_CHECK(nblk < (int64_t(1) << 31), "coord pooling: grid too large");
+    FCE_LAUNCH(pool_kernel, dim3(unsigned(nblk)), dim3(256), 0, s, xp, x.cstride, H, W, C, w.xh, w.xw, N, BPI, aff);
+  }
   int st = launch_status("coord pooling");
   if (st) return st;
   const char* nc = getenv("FCE_COORD_NO_CORE");  // diagnostics: force the split projection / attention path
@@ -1093,11 +1213,12 @@ static int coord_common(int kind, const fce_coord_desc& d, const fce_tensor& x, 
     scs = y.cstride;
   }
   _Float16* yp = static_cast<_Float16*>(y.data) + y.coff;
-  FCE_CHECK(int64_t(N) * H < 65536 * 1024, "coord attention: too many rows");
   // 4 elements per thread on wide rows (m/l 160^2 x 512: 208 -> 183 us); 1 on narrow rows, where the
   // 4-wide blocks leave too few of them (n 80^2 x 128: 22.5 vs 29 us)
   const int gpx = W * (d.oup / 8) >= 4096 ? 4 : 1;
-  const dim3 grid((W * (d.oup / 8) + 256 * gpx - 1) / (256 * gpx), N * H);
+  const int64_t gblocks = int64_t((W * (d.oup / 8) + 256 * gpx - 1) / (256 * gpx)) * N * H;
+  FCE_CHECK(gblocks < (int64_t(1) << 31), "coord attention: gate grid too large");
+  const dim3 grid{unsigned(gblocks)};
   if (kind == 0)
     FCE_LAUNCH((gpx == 4 ? gate_apply_kernel<GATE_BICOORD, 4> : gate_apply_kernel<GATE_BICOORD, 1>), grid, dim3(256), 0, s, src, scs, yp, y.cstride, N, H, W,
                        d.oup, w.g1, w.g2);
