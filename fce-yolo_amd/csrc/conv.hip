@@ -2262,10 +2262,11 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
           if (det_box ? (rc != 4 || wp != 4) : (cb > 1 && (cb >> 1) >= cotiles)) continue;
           if (n < cap) out[n++] = 0x500 | rc | (rp << 4) | (wl << 12);
         }
-  if (d.k == 1 && d.stride == 1 && !det_box && d.cin >= 64 && d.cout >= 128)  // big tiles: 0xB00 | log2(wc) << 4 | nw4
-    for (int nw4 : {0, 1})
+  if (d.k == 1 && d.stride == 1 && !det_box && d.cin >= 64 && d.cout >= 64)  // big tiles: 0xB00 | wcl << 4 | nw4 | wr4
+    for (int nwc : {0, 1, 2})  // 8 waves x 8 cout tiles, 4 x 8, 4 x 4
       for (int wcl = 0; wcl < 2; ++wcl)
-        if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xB00 | (wcl << 4) | (nw4 << 6);
+        if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles)
+          out[n++] = 0xB00 | (wcl << 4) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
   if (pipe1_ok(d, det_box))  // big-tile K-pipelined 1x1: 0x700 | log2(wp) << 12
     for (int wl = 0; wl < 3; ++wl) {
       const int cb = (4 >> wl) * 4;
@@ -2297,10 +2298,11 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int ab : {2, 3})
       for (int wm : {1, 2})
         if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
-  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 128 && !det_box && !no_gemm3())  // 0xC00
-    for (int nw4 : {0, 1})
+  if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && !no_gemm3())  // 0xC00
+    for (int nwc : {0, 1, 2})
       for (int wcl = 0; wcl < 2; ++wcl)
-        if (n < cap && ((8 << wcl) >> 1) < cotiles) out[n++] = 0xC00 | (wcl << 4) | (nw4 << 6);
+        if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles)
+          out[n++] = 0xC00 | (wcl << 4) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
   // wide tile (opt-in, FCE_WIDE3=1: measured at parity or slower on every m/l shape): 0xA00 | cwl << 4
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && wide3_on())
     for (int cwl = 0; cwl < 3; ++cwl)
@@ -2730,16 +2732,18 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     return launch_big3(a, wm, ab, nw, d.stride, x.n, s);
   }
   if (kind == 11) {  // 256-wide-tile 1x1 kernel
-    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8;
-    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0xAF) == 0 && out_kind != OUT_DFL && big1_ok(wc),
+    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8, wr = (tile >> 7) & 1 ? 4 : 8;
+    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0x2F) == 0 && out_kind != OUT_DFL && big1_ok(wc) &&
+                  (wr == 8 || nw == 4),
               "conv: bad big-tile 1x1 hint");
-    return launch_big1(a, out_kind, wc, nw, s);
+    return launch_big1(a, out_kind, wc, nw, wr, s);
   }
   if (kind == 12) {  // 256-wide-tile implicit-GEMM 3x3 kernel
-    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8;
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0xAF) == 0 && big1_ok(wc),
+    const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8, wr = (tile >> 7) & 1 ? 4 : 8;
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0x2F) == 0 && big1_ok(wc) &&
+                  (wr == 8 || nw == 4),
               "conv: bad big-tile 3x3 (implicit GEMM) hint");
-    return launch_big3g(a, wc, nw, d.stride, s);
+    return launch_big3g(a, wc, nw, wr, d.stride, s);
   }
   if (kind == 10) {  // wide-tile 3x3 kernel, per-K-step weight staging
     const int cw = 1 << ((tile >> 4) & 3);

@@ -298,11 +298,11 @@ int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hi
 // Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
 bool wide3_ok(int stride, int cw);
 int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
-// Big-tile implicit GEMM (conv_big.hip): 128 wc couts x 64 (nw / wc) pixels per nw-wave block (nw 8: one block per
-// CU; nw 4: two); 1x1 coded 0xB00 | log2(wc) << 4 | (nw == 4) << 6, 3x3 (cin % 32 == 0, stride 1 / 2, plain fp16
-// output) coded 0xC00 | log2(wc) << 4 | (nw == 4) << 6
+// Big-tile implicit GEMM (conv_big.hip): 16 wr wc couts x 64 (nw / wc) pixels per nw-wave block (nw 8: one block per
+// CU; nw 4: two; wr = cout tiles per wave, 8, or 4 with nw 4); 1x1 coded 0xB00 | log2(wc) << 4 | (nw == 4) << 6 |
+// (wr == 4) << 7, 3x3 (cin % 32 == 0, stride 1 / 2, plain fp16 output) 0xC00 | the same bits
 bool big1_ok(int wc);
-int launch_big1(const ConvArgs& a, int out_kind, int wc, int nw, hipStream_t s);
-int launch_big3g(const ConvArgs& a, int wc, int nw, int stride, hipStream_t s);
+int launch_big1(const ConvArgs& a, int out_kind, int wc, int nw, int wr, hipStream_t s);
+int launch_big3g(const ConvArgs& a, int wc, int nw, int wr, int stride, hipStream_t s);
 
 }  // namespace fce

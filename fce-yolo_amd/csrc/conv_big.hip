@@ -30,16 +30,16 @@ namespace fce {
 // stores, whole pixel rows per NSL lanes.  The fragment-layout stores (8 bytes per lane, 16 pixels x 32 bytes per
 // instruction) were the bound of this kernel: 512 -> 512 at 80^2, bs 32 ran 275 us with them and 132 us without
 // any store (FCE_BIG1_DIAG=1).  Values exactly as conv_epilogue / conv_store_staged: bitwise the same.
-template <int BC, int BP, int NT, int OUT>
-__device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8][4], int p0, int wc, int wp, int cbl0,
+template <int BC, int BP, int NT, int WR, int OUT>
+__device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[WR][4], int p0, int wc, int wp, int cbl0,
                                                   int col, int grp, _Float16* ot) {
   constexpr int ROW = BC * 16, NSL = 2 * BC;
   const int cotiles = (a.cout + 15) >> 4;
   float alpha = 1.f;
   if (OUT == OUT_WSTORE) alpha = fusion_alpha(a.fw, a.fn, a.fi);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int ctl = wc * 8 + r;
+  for (int r = 0; r < WR; ++r) {
+    const int ctl = wc * WR + r;
     const int co0 = (cbl0 + ctl) * 16 + grp * 4;
     if (cbl0 + ctl >= cotiles) continue;
     float bz[4];
@@ -90,10 +90,10 @@ __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[8
   }
 }
 
-template <int WC, int NW, int RING_>
+template <int WC, int NW, int RING_, int WR = 8>
 struct Big1Geom {
   static constexpr int WP = NW / WC;
-  static constexpr int BC = WC * 8;     // cout tiles per block
+  static constexpr int BC = WC * WR;    // cout tiles per block (WR per wave)
   static constexpr int BP = WP * 64;    // pixels per block
   static constexpr int NA = BC * 64;    // A pieces (16 B) per K-step = BC DMA instructions (1 KiB each)
   static constexpr int NB = BP * 4;     // B pieces per K-step = NB / 64 DMA instructions
@@ -105,8 +105,8 @@ struct Big1Geom {
 
 // ring slots.  8-wave blocks (one per CU): 5 when a slot is 32 KiB (WC = 2), 4 for the 40 KiB slots of WC = 1
 // (copies issued 4 / 3 steps ahead).  4-wave blocks (two per CU, 24 KiB slots): 3, so two blocks fit in the LDS and
-// one block's prologue / staged epilogue overlaps the other's K loop
-constexpr int big_ring(int wc, int nw) { return nw == 4 ? 3 : wc == 2 ? 5 : 4; }
+// one block's prologue / staged epilogue overlaps the other's K loop; with 64-cout waves (16-20 KiB slots): 4
+constexpr int big_ring(int wc, int nw, int wr = 8) { return nw == 4 ? (wr == 4 ? 4 : 3) : wc == 2 ? 5 : 4; }
 
 __device__ __forceinline__ int b1_slot(int u, int q) { return u * 4 + (q ^ ((u >> 1) & 3)); }
 
@@ -120,11 +120,14 @@ __device__ __forceinline__ void b1_glds16(const void* src, h8* lds_wave_base) {
 // K loop: the next step's fragments are read into a second register set while this step's MFMAs run, so the copies
 // are waited for one step ahead of their use (4.5-8 % over reading them after the step's barrier, l/m shapes on one
 // box; s_setprio 1 around the MFMAs measured slower)
-template <int KS, int S, int WC, int NW, int OUT, int DIAG = 0>
+// WR: cout tiles per wave, 8 (128 couts x 64 pixels) or, for 4-wave blocks, 4 (64 x 64: twice the blocks on the
+// mid-size maps of the m/l scales, 0.5 KiB of fragment reads per MFMA)
+template <int KS, int S, int WC, int NW, int OUT, int DIAG = 0, int WR = 8>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(ConvArgs a) {
   static_assert(KS == 1 ? S == 1 : (KS == 3 && (S == 1 || S == 2)), "conv big tile: 1x1 s1 or 3x3 s1 / s2");
   static_assert(NW == 8 || NW == 4, "conv big tile: 8- or 4-wave blocks");
-  using G = Big1Geom<WC, NW, big_ring(WC, NW)>;
+  static_assert(WR == 8 || (WR == 4 && NW == 4), "conv big tile: 64-cout waves in 4-wave blocks only");
+  using G = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR>;
   constexpr int WP = G::WP, BC = G::BC, BP = G::BP, NA = G::NA, NB = G::NB, IA = G::IA, IB = G::IB, RING = G::RING;
   extern __shared__ __attribute__((aligned(16))) h8 big1_smem[];  // RING x [A | B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -215,34 +218,34 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
     }
   };
 
-  f4 acc[8][4];
+  f4 acc[WR][4];
 #pragma unroll
-  for (int r = 0; r < 8; ++r)
+  for (int r = 0; r < WR; ++r)
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: steps 0 .. RING - 2 in flight (copies past nst read zero weight steps / zero pixels: harmless)
 #pragma unroll
   for (int t = 0; t < RING - 1; ++t) issue(t);
-  auto frags = [&](int t, h8(&fa)[8], h8(&fb)[4]) {
+  auto frags = [&](int t, h8(&fa)[WR], h8(&fb)[4]) {
     const h8* cur = big1_smem + (t % RING) * (NA + NB);
 #pragma unroll
     for (int p = 0; p < 4; ++p) fb[p] = cur[NA + b1_slot(wp * 64 + p * 16 + col, grp)];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) fa[r] = cur[(wc * 8 + r) * 64 + lane];
+    for (int r = 0; r < WR; ++r) fa[r] = cur[(wc * WR + r) * 64 + lane];
   };
   // step s: step s + 1's copies landed (steps s + 2 .. s + RING - 2 may stay in flight) and published; step
   // s + RING - 1 issued into the slot step s - 1 used (its fragments were read during step s - 2 and consumed by
   // step s - 1's MFMAs, which every wave finished before this barrier); step s + 1's fragments read into the
   // other register set while step s's MFMAs run from this one
-  auto step = [&](int s, h8(&ca)[8], h8(&cb)[4], h8(&na)[8], h8(&nb)[4]) {
+  auto step = [&](int s, h8(&ca)[WR], h8(&cb)[4], h8(&na)[WR], h8(&nb)[4]) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 3) * (IA + IB)) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (DIAG != 2) issue(s + RING - 1);
     frags(s + 1, na, nb);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < WR; ++r) {
       if (DIAG == 3) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) acc[r][p][0] += (float)ca[r][p] + (float)cb[p][r];
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
       for (int p = 0; p < 4; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ca[r], cb[p], acc[r][p], 0, 0, 0);
     }
   };
-  h8 a0[8], b0[4], a1[8], b1[4];
+  h8 a0[WR], b0[4], a1[WR], b1[4];
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (IA + IB)) : "memory");  // step 0 landed
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
   if (DIAG == 1) {
     float t = 0.f;
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
+    for (int r = 0; r < WR; ++r)
 #pragma unroll
       for (int p = 0; p < 4; ++p) t += acc[r][p][0] + acc[r][p][1] + acc[r][p][2] + acc[r][p][3];
     if (t == 1234.5678f) static_cast<_Float16*>(a.y)[tid] = (_Float16)t;
@@ -277,29 +280,30 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
     if (a.stg) {  // the ring is free once every wave is past its last step (BP x BC*16 halves fit in it)
       static_assert(size_t(BP) * BC * 16 * 2 <= G::lds, "staged output tile exceeds the ring");
       __syncthreads();
-      big1_store_staged<BC, BP, NW * 64, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
+      big1_store_staged<BC, BP, NW * 64, WR, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
       return;
     }
   }
-  conv_epilogue<8, 4, OUT>(a, acc, p0 + wp * 64, ct_blk + wc * 8, col, grp);
+  conv_epilogue<WR, 4, OUT>(a, acc, p0 + wp * 64, ct_blk + wc * WR, col, grp);
 }
 
 bool big1_ok(int wc) { return wc == 1 || wc == 2; }
 
-template <int KS, int S, int WC, int NW, int OUT, int DIAG>
+template <int KS, int S, int WC, int NW, int OUT, int DIAG, int WR = 8>
 static int launch_big_d(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr size_t lds = Big1Geom<WC, NW, big_ring(WC, NW)>::lds;
+  constexpr size_t lds = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR>::lds;
   static_assert(lds * (NW == 4 ? 2 : 1) <= 160 * 1024, "big tile: LDS over 160 KiB per CU");
   static const bool big =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, NW, OUT, DIAG>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!big) return fail(FCE_ERR_HIP, "conv big tile: cannot opt in to >64 KiB LDS");
-  FCE_LAUNCH((conv_big_kernel<KS, S, WC, NW, OUT, DIAG>), grid, dim3(NW * 64), lds, s, a);
+  FCE_LAUNCH((conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR>), grid, dim3(NW * 64), lds, s, a);
   return FCE_OK;
 }
 
-template <int KS, int S, int WC, int NW, int OUT>
+template <int KS, int S, int WC, int NW, int OUT, int WR = 8>
 static int launch_big_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (WR == 4) return launch_big_d<KS, S, WC, NW, OUT, 0, 4>(a, grid, s);
   static const int diag = [] {
     const char* e = getenv("FCE_BIG1_DIAG");
     return e ? atoi(e) : 0;
@@ -312,58 +316,65 @@ static int launch_big_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
   return launch_big_d<KS, S, WC, NW, OUT, 0>(a, grid, s);
 }
 
-template <int WC, int NW>
+template <int WC, int NW, int WR = 8>
 static int launch_big1_w(const ConvArgs& a, int out_kind, dim3 grid, hipStream_t s) {
   switch (out_kind) {
-    case OUT_F16: return launch_big_k<1, 1, WC, NW, OUT_F16>(a, grid, s);
-    case OUT_F32: return launch_big_k<1, 1, WC, NW, OUT_F32>(a, grid, s);
-    case OUT_WSTORE: return launch_big_k<1, 1, WC, NW, OUT_WSTORE>(a, grid, s);
-    case OUT_ACCUM: return launch_big_k<1, 1, WC, NW, OUT_ACCUM>(a, grid, s);
-    case OUT_CLS: return launch_big_k<1, 1, WC, NW, OUT_CLS>(a, grid, s);
+    case OUT_F16: return launch_big_k<1, 1, WC, NW, OUT_F16, WR>(a, grid, s);
+    case OUT_F32: return launch_big_k<1, 1, WC, NW, OUT_F32, WR>(a, grid, s);
+    case OUT_WSTORE: return launch_big_k<1, 1, WC, NW, OUT_WSTORE, WR>(a, grid, s);
+    case OUT_ACCUM: return launch_big_k<1, 1, WC, NW, OUT_ACCUM, WR>(a, grid, s);
+    case OUT_CLS: return launch_big_k<1, 1, WC, NW, OUT_CLS, WR>(a, grid, s);
     default: return fail(FCE_ERR_INVALID, "conv 1x1 big tile: unsupported epilogue");
   }
 }
 
-static ConvArgs big_grid(const ConvArgs& a0, int wc, int nw, dim3& grid) {
+static ConvArgs big_grid(const ConvArgs& a0, int wc, int nw, int wr, dim3& grid) {
   ConvArgs a = a0;
-  const int bp = (nw / wc) * 64, bc = wc * 8;
+  const int bp = (nw / wc) * 64, bc = wc * wr;
   a.gy = ((a.cout + 15) / 16 + bc - 1) / bc;
   const int64_t tiles = (int64_t(a.P) + bp - 1) / bp;
   grid = dim3(unsigned(std::min<int64_t>(tiles * a.gy, int64_t(1) << 31)));
   return a;
 }
 
-int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, hipStream_t s) {
-  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && a0.cin % 8 == 0 && out_kind != OUT_DFL,
+int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, int wr, hipStream_t s) {
+  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && (wr == 8 || (wr == 4 && nw == 4)) && a0.cin % 8 == 0 &&
+                out_kind != OUT_DFL,
             "conv 1x1 big tile: bad configuration");
   dim3 grid;
-  const ConvArgs a = big_grid(a0, wc, nw, grid);
+  const ConvArgs a = big_grid(a0, wc, nw, wr, grid);
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 1x1 big tile: grid too large");
   int rc;
   if (nw == 8)
     rc = wc == 1 ? launch_big1_w<1, 8>(a, out_kind, grid, s) : launch_big1_w<2, 8>(a, out_kind, grid, s);
-  else
+  else if (wr == 8)
     rc = wc == 1 ? launch_big1_w<1, 4>(a, out_kind, grid, s) : launch_big1_w<2, 4>(a, out_kind, grid, s);
+  else
+    rc = wc == 1 ? launch_big1_w<1, 4, 4>(a, out_kind, grid, s) : launch_big1_w<2, 4, 4>(a, out_kind, grid, s);
   if (rc != FCE_OK) return rc;
   return launch_status("conv_big_kernel");
 }
 
-template <int S, int NW>
+template <int S, int NW, int WR>
 static int launch_big3g_s(const ConvArgs& a, int wc, dim3 grid, hipStream_t s) {
-  return wc == 1 ? launch_big_k<3, S, 1, NW, OUT_F16>(a, grid, s) : launch_big_k<3, S, 2, NW, OUT_F16>(a, grid, s);
+  return wc == 1 ? launch_big_k<3, S, 1, NW, OUT_F16, WR>(a, grid, s)
+                 : launch_big_k<3, S, 2, NW, OUT_F16, WR>(a, grid, s);
 }
 
-int launch_big3g(const ConvArgs& a0, int wc, int nw, int stride, hipStream_t s) {
-  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && a0.cin % 32 == 0 && a0.up == 0 && (stride == 1 || stride == 2),
+int launch_big3g(const ConvArgs& a0, int wc, int nw, int wr, int stride, hipStream_t s) {
+  FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && (wr == 8 || (wr == 4 && nw == 4)) && a0.cin % 32 == 0 &&
+                a0.up == 0 && (stride == 1 || stride == 2),
             "conv 3x3 big tile: bad configuration");
   dim3 grid;
-  const ConvArgs a = big_grid(a0, wc, nw, grid);
+  const ConvArgs a = big_grid(a0, wc, nw, wr, grid);
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 3x3 big tile: grid too large");
   int rc;
   if (stride == 1)
-    rc = nw == 8 ? launch_big3g_s<1, 8>(a, wc, grid, s) : launch_big3g_s<1, 4>(a, wc, grid, s);
+    rc = nw == 8 ? launch_big3g_s<1, 8, 8>(a, wc, grid, s)
+                 : wr == 8 ? launch_big3g_s<1, 4, 8>(a, wc, grid, s) : launch_big3g_s<1, 4, 4>(a, wc, grid, s);
   else
-    rc = nw == 8 ? launch_big3g_s<2, 8>(a, wc, grid, s) : launch_big3g_s<2, 4>(a, wc, grid, s);
+    rc = nw == 8 ? launch_big3g_s<2, 8, 8>(a, wc, grid, s)
+                 : wr == 8 ? launch_big3g_s<2, 4, 8>(a, wc, grid, s) : launch_big3g_s<2, 4, 4>(a, wc, grid, s);
   if (rc != FCE_OK) return rc;
   return launch_status("conv_big_kernel");
 }
