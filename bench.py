@@ -14,10 +14,13 @@ A step = one global batch of B images per GPU through `dist.ShardedPredictor`: e
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
 with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
-default three batches are in flight per GPU (--lanes 3, engine.Pipeline lanes): three executors with their
-own arenas on three streams, each running forward then NMS of every third batch, so one batch's
-latency-bound coarse layers and NMS share the CUs with the next batch's full-width layers; the gather
-runs on a side stream in batch order.  --lanes 1 keeps one executor (the NMS of batch i on a side stream
+default four batches are in flight per GPU (--lanes 4, engine.Pipeline lanes): four executors with their
+own arenas on four streams, each running forward then NMS of every fourth batch, so one batch's
+latency-bound coarse layers and NMS share the CUs with the next batches' full-width layers; the gather
+runs on a side stream in batch order.  With four lanes the process asks HIP for 8 hardware queues
+(GPU_MAX_HW_QUEUES, set before torch is imported; HIP's default 4 is shared by the lanes, the side stream and
+the default stream): 4 lanes x 8 queues 29.3-29.6k against 28.7-28.8k images/s for 3 lanes x 4 queues,
+interleaved on one box (profiles/r03w_lanes_queues.txt).  --lanes 1 keeps one executor (the NMS of batch i on a side stream
 under the forward of batch i+1); --sequential runs forward and NMS back to back.  Weights are the portable seeded weights of the named
 architecture (no checkpoints offline), broadcast from rank 0 over RCCL.  Per-GPU work is fixed as N
 grows: scaling is weak.  Prints ONE JSON line on rank 0.
@@ -50,7 +53,24 @@ def launch_command(argv, env):
             "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
 
 
+DEFAULT_LANES = 4
+
+
+def hw_queues_env(argv, env):
+    """HIP hardware queues for `--lanes` >= 4: at least 8 (the lanes' streams, the NMS / gather side stream and
+    the default stream would share HIP's default 4).  Returns the value to export, or None to leave the
+    environment alone.  Pure: runs before torch is imported (HIP reads it when it initialises)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--lanes", type=int, default=int(env.get("FCE_LANES", DEFAULT_LANES)))
+    a, _ = pre.parse_known_args(argv)
+    have = int(env.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    return "8" if a.lanes >= 4 and have < 8 else None
+
+
 if __name__ == "__main__":
+    _q = hw_queues_env(sys.argv[1:], os.environ)
+    if _q is not None:
+        os.environ["GPU_MAX_HW_QUEUES"] = _q
     _cmd = launch_command(sys.argv[1:], os.environ)
     if _cmd is not None:  # launcher: start the ranks as a child process (never exec), exit with its status
         if os.environ.get("FCE_BENCH_DRY_LAUNCH") == "1":
@@ -110,7 +130,7 @@ def parse_args():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
     ap.add_argument("--sequential", action="store_true", help="forward then NMS on one stream (no overlap)")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FCE_LANES", "3")),
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FCE_LANES", DEFAULT_LANES)),
                     help="batches in flight per GPU (engine.Pipeline lanes: one executor + stream each)")
     ap.add_argument("--graph", type=int, default=-1, help="1: replay a captured hipGraph per lane; 0: direct "
                     "launches; -1 (default): replay when lanes > 1 (ties direct launches there, 28.2k both; with one "
@@ -379,6 +399,7 @@ def main():
         "config": {"workload": f"{stem} detection inference (forward + decode + NMS) @ {S}x{S}, {B} images/GPU",
                    "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}",
                    "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes,
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                    "forward_launch": "hipgraph" if a.graph else "direct"},
         "roofline": roof,
         "roofline_forward": {"achieved": round(ach_tfs, 3), "peak": round(roof_tfs, 2), "unit": "TFLOP/s",

@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}  # the bench default (4 lanes) asks for 8; set before rocprofv3 starts the program
 TAG=${1:-r01}
 shift
 STEPS=20

@@ -482,7 +482,8 @@ def test_fused_best_class_keys_match_pred_and_nms(device):
         assert torch.equal(n1.buf, n2.buf)
 
 
-@pytest.mark.parametrize("defer,lanes,graph", [(True, 1, False), (False, 1, False), (False, 2, False), (False, 3, True)])
+@pytest.mark.parametrize("defer,lanes,graph", [(True, 1, False), (False, 1, False), (False, 2, False), (False, 3, True),
+                                               (False, 4, True)])
 def test_pipeline_overlap_matches_sequential(defer, lanes, graph, device):
     """engine.Pipeline (forward i+1 overlapping NMS i, double-buffered; deferred to the next forward's
     fork point or right after the forward; or 2-3 lanes = executors on their own streams with batches

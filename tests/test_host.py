@@ -243,6 +243,10 @@ def test_bench_gpus_n_launches_ranks_before_torch():
     assert m.launch_command(["--gpus", "8"], {"WORLD_SIZE": "8"}) is None
     assert m.launch_command(["--gpus", "1"], {}) is None
     assert m.launch_command([], {}) is None
+    # hardware queues: 8 for the default 4 lanes unless the environment already asks for >= 8; 3 lanes: untouched
+    assert m.hw_queues_env([], {}) == "8" and m.hw_queues_env([], {"GPU_MAX_HW_QUEUES": "4"}) == "8"
+    assert m.hw_queues_env([], {"GPU_MAX_HW_QUEUES": "16"}) is None
+    assert m.hw_queues_env(["--lanes", "3"], {}) is None and m.hw_queues_env([], {"FCE_LANES": "2"}) is None
 
 
 def test_bench_world_size_mismatch_fails():
