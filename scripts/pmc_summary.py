@@ -28,6 +28,12 @@ def family(name):
         if out == 5:
             return "conv1x1_detect_cls"
         return "conv3x3_mfma" if ks == 3 else "conv1x1_mfma"
+    m = re.search(r"conv_big_kernel<(\d), \d+, \d+, \d+, (\d)", name)  # 256-wide implicit GEMM (1x1 / 3x3)
+    if m:
+        ks, out = int(m.group(1)), int(m.group(2))
+        if out == 5:
+            return "conv1x1_detect_cls"
+        return "conv3x3_mfma" if ks == 3 else "conv1x1_mfma"
     m = re.search(r"conv1x1_(?:lds|ring)_kernel<\d+, \d+, \d+, \d+, (\d)>", name) or \
         re.search(r"conv1x1_stream_kernel<\d+, \d+, \d+, (\d)>", name)
     if m:
@@ -37,6 +43,7 @@ def family(name):
                      ("conv1x1_pipe", "conv1x1_mfma"), ("stem", "conv_stem"), ("psa_attention", "psa_attention"),
                      ("dwconv", "dwconv3x3"), ("maxpool", "maxpool_chain"), ("weighted_add", "bifpn_weighted_add"),
                      ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"), ("pool_kernel", "bicoordcrossatt"),
+                     ("pool_band", "bicoordcrossatt"), ("conv3x3_wide", "conv3x3_mfma"),
                      ("coord_", "bicoordcrossatt"), ("gate_apply", "bicoordcrossatt"), ("nms", "nms"),
                      ("detect_decode", "detect_decode"), ("c3k2_fused", "c3k2_fused")):
         if key in name:
