@@ -14,8 +14,8 @@ A step = one global batch of B images per GPU through `dist.ShardedPredictor`: e
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
 with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
-default four batches are in flight per GPU (--lanes 4, engine.Pipeline lanes): four executors with their
-own arenas on four streams, each running forward then NMS of every fourth batch, so one batch's
+default four batches are in flight per GPU on the n scale and three on the wider ones (--lanes, engine.Pipeline
+lanes): executors with their own arenas on their own streams, each running forward then NMS of every L-th batch, so one batch's
 latency-bound coarse layers and NMS share the CUs with the next batches' full-width layers; the gather
 runs on a side stream in batch order.  With four lanes the process asks HIP for 8 hardware queues
 (GPU_MAX_HW_QUEUES, set before torch is imported; HIP's default 4 is shared by the lanes, the side stream and
@@ -53,18 +53,28 @@ def launch_command(argv, env):
             "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
 
 
-DEFAULT_LANES = 4
+def default_lanes(model: str, env) -> int:
+    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n scale (its four activation
+    arenas still fit the 256 MB MALL: 29.3-29.6k vs 28.7-28.8k images/s with 3) and 3 for the wider scales (l32
+    4 954 vs 4 573, m16-h8 1 625 vs 1 529 images/s with 4, profiles/r03y_*)."""
+    if env.get("FCE_LANES"):
+        return int(env["FCE_LANES"])
+    stem = Path(model).stem
+    scale = stem[6:7] if stem.startswith("yolo11") else ""
+    return 4 if scale == "n" else 3
 
 
 def hw_queues_env(argv, env):
-    """HIP hardware queues for `--lanes` >= 4: at least 8 (the lanes' streams, the NMS / gather side stream and
+    """HIP hardware queues for 4 or more lanes: at least 8 (the lanes' streams, the NMS / gather side stream and
     the default stream would share HIP's default 4).  Returns the value to export, or None to leave the
     environment alone.  Pure: runs before torch is imported (HIP reads it when it initialises)."""
     pre = argparse.ArgumentParser(add_help=False)
-    pre.add_argument("--lanes", type=int, default=int(env.get("FCE_LANES", DEFAULT_LANES)))
+    pre.add_argument("--model", default="yolo11n-fce.yaml")
+    pre.add_argument("--lanes", type=int, default=None)
     a, _ = pre.parse_known_args(argv)
+    lanes = a.lanes if a.lanes is not None else default_lanes(a.model, env)
     have = int(env.get("GPU_MAX_HW_QUEUES", "4") or 4)
-    return "8" if a.lanes >= 4 and have < 8 else None
+    return "8" if lanes >= 4 and have < 8 else None
 
 
 if __name__ == "__main__":
@@ -130,8 +140,9 @@ def parse_args():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--no-nms", action="store_true", help="time the forward only")
     ap.add_argument("--sequential", action="store_true", help="forward then NMS on one stream (no overlap)")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("FCE_LANES", DEFAULT_LANES)),
-                    help="batches in flight per GPU (engine.Pipeline lanes: one executor + stream each)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="batches in flight per GPU (engine.Pipeline lanes: one executor + stream each; default "
+                         "FCE_LANES, else 4 for the n scale and 3 for the others)")
     ap.add_argument("--graph", type=int, default=-1, help="1: replay a captured hipGraph per lane; 0: direct "
                     "launches; -1 (default): replay when lanes > 1 (ties direct launches there, 28.2k both; with one "
                     "lane direct launches are faster, DESIGN.md)")
@@ -142,6 +153,8 @@ def parse_args():
     ap.add_argument("--predict-steps", type=int, default=30,
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
     a = ap.parse_args()
+    if a.lanes is None:
+        a.lanes = default_lanes(a.model, os.environ)
     if a.graph < 0:
         a.graph = 1 if a.lanes > 1 else 0
     return a

@@ -2263,10 +2263,12 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
           if (n < cap) out[n++] = 0x500 | rc | (rp << 4) | (wl << 12);
         }
   if (d.k == 1 && d.stride == 1 && !det_box && d.cin >= 64 && d.cout >= 64)  // big tiles: 0xB00 | wcl << 4 | nw4 | wr4
-    for (int nwc : {0, 1, 2})  // 8 waves x 8 cout tiles, 4 x 8, 4 x 4
-      for (int wcl = 0; wcl < 2; ++wcl)
-        if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles)
-          out[n++] = 0xB00 | (wcl << 4) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
+    for (int split : {0, 1})   // one ring, or split rings with a deep pixel ring (0x20)
+      for (int nwc : {0, 1, 2})  // 8 waves x 8 cout tiles, 4 x 8, 4 x 4
+        for (int wcl = 0; wcl < 2; ++wcl)
+          if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles &&
+              (!split || big1_split_ok(1 << wcl, nwc ? 4 : 8, nwc == 2 ? 4 : 8)))
+            out[n++] = 0xB00 | (wcl << 4) | (split << 5) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
   if (pipe1_ok(d, det_box))  // big-tile K-pipelined 1x1: 0x700 | log2(wp) << 12
     for (int wl = 0; wl < 3; ++wl) {
       const int cb = (4 >> wl) * 4;
@@ -2733,10 +2735,10 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   }
   if (kind == 11) {  // 256-wide-tile 1x1 kernel
     const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8, wr = (tile >> 7) & 1 ? 4 : 8;
-    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0x2F) == 0 && out_kind != OUT_DFL && big1_ok(wc) &&
+    FCE_CHECK(d.k == 1 && d.stride == 1 && (tile & 0x0F) == 0 && out_kind != OUT_DFL && big1_ok(wc) &&
                   (wr == 8 || nw == 4),
               "conv: bad big-tile 1x1 hint");
-    return launch_big1(a, out_kind, wc, nw, wr, s);
+    return launch_big1(a, out_kind, wc, nw, wr, (tile >> 5) & 1, s);
   }
   if (kind == 12) {  // 256-wide-tile implicit-GEMM 3x3 kernel
     const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8, wr = (tile >> 7) & 1 ? 4 : 8;

@@ -302,7 +302,8 @@ int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
 // CU; nw 4: two; wr = cout tiles per wave, 8, or 4 with nw 4); 1x1 coded 0xB00 | log2(wc) << 4 | (nw == 4) << 6 |
 // (wr == 4) << 7, 3x3 (cin % 32 == 0, stride 1 / 2, plain fp16 output) 0xC00 | the same bits
 bool big1_ok(int wc);
-int launch_big1(const ConvArgs& a, int out_kind, int wc, int nw, int wr, hipStream_t s);
+bool big1_split_ok(int wc, int nw, int wr);
+int launch_big1(const ConvArgs& a, int out_kind, int wc, int nw, int wr, bool split, hipStream_t s);  // split: | 0x20
 int launch_big3g(const ConvArgs& a, int wc, int nw, int wr, int stride, hipStream_t s);
 
 }  // namespace fce

@@ -90,7 +90,7 @@ __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[W
   }
 }
 
-template <int WC, int NW, int RING_, int WR = 8>
+template <int WC, int NW, int RING_, int WR = 8, int RBD = 0>
 struct Big1Geom {
   static constexpr int WP = NW / WC;
   static constexpr int BC = WC * WR;    // cout tiles per block (WR per wave)
@@ -99,8 +99,12 @@ struct Big1Geom {
   static constexpr int NB = BP * 4;     // B pieces per K-step = NB / 64 DMA instructions
   static constexpr int IA = BC / NW, IB = NB / 64 / NW;  // DMA instructions per wave per K-step
   static constexpr int RING = RING_;    // K-step slots: the copies of step s + RING - 1 go out while step s computes
-  static constexpr size_t lds = size_t(RING) * (NA + NB) * 16;
+  // split rings (RBD > 0, the HBM-bound 1x1s): the weights (L2 hits) in a 3-slot ring issued 2 steps ahead, the
+  // pixels (HBM) in an RBD-slot ring issued RBD - 1 steps ahead
+  static constexpr int RA = RBD ? 3 : RING, RB = RBD ? RBD : RING;
+  static constexpr size_t lds = RBD ? size_t(RA * NA + RB * NB) * 16 : size_t(RING) * (NA + NB) * 16;
   static_assert(BC % NW == 0 && (NB / 64) % NW == 0, "whole DMA rounds per wave");
+  static_assert(RBD == 0 || RBD >= 4, "split rings: the pixel ring at least 4 deep");
 };
 
 // ring slots.  8-wave blocks (one per CU): 5 when a slot is 32 KiB (WC = 2), 4 for the 40 KiB slots of WC = 1
@@ -122,13 +126,14 @@ __device__ __forceinline__ void b1_glds16(const void* src, h8* lds_wave_base) {
 // box; s_setprio 1 around the MFMAs measured slower)
 // WR: cout tiles per wave, 8 (128 couts x 64 pixels) or, for 4-wave blocks, 4 (64 x 64: twice the blocks on the
 // mid-size maps of the m/l scales, 0.5 KiB of fragment reads per MFMA)
-template <int KS, int S, int WC, int NW, int OUT, int DIAG = 0, int WR = 8>
+template <int KS, int S, int WC, int NW, int OUT, int DIAG = 0, int WR = 8, int RBD = 0>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(ConvArgs a) {
   static_assert(KS == 1 ? S == 1 : (KS == 3 && (S == 1 || S == 2)), "conv big tile: 1x1 s1 or 3x3 s1 / s2");
   static_assert(NW == 8 || NW == 4, "conv big tile: 8- or 4-wave blocks");
   static_assert(WR == 8 || (WR == 4 && NW == 4), "conv big tile: 64-cout waves in 4-wave blocks only");
-  using G = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR>;
+  using G = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR, RBD>;
   constexpr int WP = G::WP, BC = G::BC, BP = G::BP, NA = G::NA, NB = G::NB, IA = G::IA, IB = G::IB, RING = G::RING;
+  constexpr int RA = G::RA, RB = G::RB;
   extern __shared__ __attribute__((aligned(16))) h8 big1_smem[];  // RING x [A | B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, grp = lane >> 4;
@@ -187,16 +192,23 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
   // and waits lgkmcnt(0) for it, which also waits for the next step's fragment reads in flight
   const void* zl = g_zero_line;
   asm volatile("" : "+s"(zl));
-  auto issue = [&](int t) {  // step t's copies into ring slot t % RING
-    h8* slot = big1_smem + (t % RING) * (NA + NB);
+  // ring slots of step t: one ring of (A | B) slots, or (RBD) an A ring and a deeper B ring
+  auto slot_a = [&](int t) -> h8* { return RBD ? big1_smem + (t % RA) * NA : big1_smem + (t % RING) * (NA + NB); };
+  auto slot_b = [&](int t) -> h8* {
+    return RBD ? big1_smem + RA * NA + (t % RB) * NB : big1_smem + (t % RING) * (NA + NB) + NA;
+  };
+  auto issue_a = [&](int t) {  // step t's weight copies
+    h8* slot = slot_a(t);
 #pragma unroll
     for (int j = 0; j < IA; ++j) b1_glds16(asrc[j] + size_t(t) * 64, slot + (wave + NW * j) * 64);  // zero steps past nst
+  };
+  auto issue_b = [&](int t) {  // step t's pixel copies (called in step order: the 3x3 tap cursor advances)
+    h8* slot = slot_b(t);
     if constexpr (KS == 1) {
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
         const bool ok = boff[j] >= 0 && t * 32 + bq[j] < a.cin;
-        b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + t * 32) : zl,
-                  slot + NA + (wave + NW * j) * 64);
+        b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + t * 32) : zl, slot + (wave + NW * j) * 64);
       }
     } else {
       const int64_t toff = int64_t(iky * a.Ws + ikx) * a.xcs + ic * 32;
@@ -205,8 +217,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
         const bool ok = live && (bm[j] & need) == need;
-        b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + toff) : zl,
-                  slot + NA + (wave + NW * j) * 64);
+        b1_glds16(ok ? static_cast<const void*>(a.x + boff[j] + toff) : zl, slot + (wave + NW * j) * 64);
       }
       if (++ikx == 3) {
         ikx = 0;
@@ -217,6 +228,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
       }
     }
   };
+  auto issue = [&](int t) {  // one ring: step t's copies, A then B
+    issue_a(t);
+    issue_b(t);
+  };
 
   f4 acc[WR][4];
 #pragma unroll
@@ -224,25 +239,47 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: steps 0 .. RING - 2 in flight (copies past nst read zero weight steps / zero pixels: harmless)
+  // prologue: steps 0 .. RING - 2 in flight (copies past nst read zero weight steps / zero pixels: harmless).
+  // Split rings: A(0), B(0), A(1), B(1), B(2) .. B(RB - 2)
+  if constexpr (RBD) {
 #pragma unroll
-  for (int t = 0; t < RING - 1; ++t) issue(t);
+    for (int t = 0; t < RB - 1; ++t) {
+      if (t < RA - 1) issue_a(t);
+      issue_b(t);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < RING - 1; ++t) issue(t);
+  }
   auto frags = [&](int t, h8(&fa)[WR], h8(&fb)[4]) {
-    const h8* cur = big1_smem + (t % RING) * (NA + NB);
+    const h8* ca = slot_a(t);
+    const h8* cb = slot_b(t);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) fb[p] = cur[NA + b1_slot(wp * 64 + p * 16 + col, grp)];
+    for (int p = 0; p < 4; ++p) fb[p] = cb[b1_slot(wp * 64 + p * 16 + col, grp)];
 #pragma unroll
-    for (int r = 0; r < WR; ++r) fa[r] = cur[(wc * WR + r) * 64 + lane];
+    for (int r = 0; r < WR; ++r) fa[r] = ca[(wc * WR + r) * 64 + lane];
   };
+  // copies a wave may leave in flight at step s's wait (step s + 1's must have landed; vmcnt retires in issue
+  // order).  One ring: the RING - 3 later steps.  Split rings: A(s + 1) went out at step s - 1 followed only by
+  // B(s + RB - 2); early steps wait for more than needed (their later copies are all B's of the prologue)
+  constexpr int ALLOW = RBD ? IB : (RING - 3) * (IA + IB);
+  constexpr int ALLOW0 = RBD ? IA + (RB - 2) * IB : (RING - 2) * (IA + IB);  // before step 0
   // step s: step s + 1's copies landed (steps s + 2 .. s + RING - 2 may stay in flight) and published; step
   // s + RING - 1 issued into the slot step s - 1 used (its fragments were read during step s - 2 and consumed by
   // step s - 1's MFMAs, which every wave finished before this barrier); step s + 1's fragments read into the
   // other register set while step s's MFMAs run from this one
   auto step = [&](int s, h8(&ca)[WR], h8(&cb)[4], h8(&na)[WR], h8(&nb)[4]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 3) * (IA + IB)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALLOW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (DIAG != 2) issue(s + RING - 1);
+    if (DIAG != 2) {
+      if constexpr (RBD) {
+        issue_a(s + RA - 1);
+        issue_b(s + RB - 1);
+      } else {
+        issue(s + RING - 1);
+      }
+    }
     frags(s + 1, na, nb);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
@@ -256,7 +293,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
     }
   };
   h8 a0[WR], b0[4], a1[WR], b1[4];
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (IA + IB)) : "memory");  // step 0 landed
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALLOW0) : "memory");  // step 0 landed
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   frags(0, a0, b0);
@@ -278,7 +315,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
   }
   if constexpr (OUT == OUT_F16 || OUT == OUT_WSTORE) {
     if (a.stg) {  // the ring is free once every wave is past its last step (BP x BC*16 halves fit in it)
-      static_assert(size_t(BP) * BC * 16 * 2 <= G::lds, "staged output tile exceeds the ring");
+      static_assert(size_t(BP) * BC * 16 * 2 <= G::lds, "staged output tile exceeds the rings");
       __syncthreads();
       big1_store_staged<BC, BP, NW * 64, WR, OUT>(a, acc, p0, wc, wp, ct_blk, col, grp, reinterpret_cast<_Float16*>(big1_smem));
       return;
@@ -289,21 +326,21 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_big_kernel(Conv
 
 bool big1_ok(int wc) { return wc == 1 || wc == 2; }
 
-template <int KS, int S, int WC, int NW, int OUT, int DIAG, int WR = 8>
+template <int KS, int S, int WC, int NW, int OUT, int DIAG, int WR = 8, int RBD = 0>
 static int launch_big_d(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr size_t lds = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR>::lds;
+  constexpr size_t lds = Big1Geom<WC, NW, big_ring(WC, NW, WR), WR, RBD>::lds;
   static_assert(lds * (NW == 4 ? 2 : 1) <= 160 * 1024, "big tile: LDS over 160 KiB per CU");
   static const bool big =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR, RBD>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!big) return fail(FCE_ERR_HIP, "conv big tile: cannot opt in to >64 KiB LDS");
-  FCE_LAUNCH((conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR>), grid, dim3(NW * 64), lds, s, a);
+  FCE_LAUNCH((conv_big_kernel<KS, S, WC, NW, OUT, DIAG, WR, RBD>), grid, dim3(NW * 64), lds, s, a);
   return FCE_OK;
 }
 
-template <int KS, int S, int WC, int NW, int OUT, int WR = 8>
+template <int KS, int S, int WC, int NW, int OUT, int WR = 8, int RBD = 0>
 static int launch_big_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if constexpr (WR == 4) return launch_big_d<KS, S, WC, NW, OUT, 0, 4>(a, grid, s);
+  if constexpr (WR == 4 || RBD) return launch_big_d<KS, S, WC, NW, OUT, 0, WR, RBD>(a, grid, s);
   static const int diag = [] {
     const char* e = getenv("FCE_BIG1_DIAG");
     return e ? atoi(e) : 0;
@@ -316,14 +353,14 @@ static int launch_big_k(const ConvArgs& a, dim3 grid, hipStream_t s) {
   return launch_big_d<KS, S, WC, NW, OUT, 0>(a, grid, s);
 }
 
-template <int WC, int NW, int WR = 8>
+template <int WC, int NW, int WR = 8, int RBD = 0>
 static int launch_big1_w(const ConvArgs& a, int out_kind, dim3 grid, hipStream_t s) {
   switch (out_kind) {
-    case OUT_F16: return launch_big_k<1, 1, WC, NW, OUT_F16, WR>(a, grid, s);
-    case OUT_F32: return launch_big_k<1, 1, WC, NW, OUT_F32, WR>(a, grid, s);
-    case OUT_WSTORE: return launch_big_k<1, 1, WC, NW, OUT_WSTORE, WR>(a, grid, s);
-    case OUT_ACCUM: return launch_big_k<1, 1, WC, NW, OUT_ACCUM, WR>(a, grid, s);
-    case OUT_CLS: return launch_big_k<1, 1, WC, NW, OUT_CLS, WR>(a, grid, s);
+    case OUT_F16: return launch_big_k<1, 1, WC, NW, OUT_F16, WR, RBD>(a, grid, s);
+    case OUT_F32: return launch_big_k<1, 1, WC, NW, OUT_F32, WR, RBD>(a, grid, s);
+    case OUT_WSTORE: return launch_big_k<1, 1, WC, NW, OUT_WSTORE, WR, RBD>(a, grid, s);
+    case OUT_ACCUM: return launch_big_k<1, 1, WC, NW, OUT_ACCUM, WR, RBD>(a, grid, s);
+    case OUT_CLS: return launch_big_k<1, 1, WC, NW, OUT_CLS, WR, RBD>(a, grid, s);
     default: return fail(FCE_ERR_INVALID, "conv 1x1 big tile: unsupported epilogue");
   }
 }
@@ -337,7 +374,14 @@ static ConvArgs big_grid(const ConvArgs& a0, int wc, int nw, int wr, dim3& grid)
   return a;
 }
 
-int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, int wr, hipStream_t s) {
+// the deep pixel ring (split rings) of each 1x1 configuration: as deep as the LDS allows (one block per CU for 8
+// waves, two for 4), 0 = one ring
+static constexpr int big1_rbd(int wc, int nw, int wr) {
+  return nw == 8 ? (wc == 2 ? 6 : 4) : wr == 4 ? (wc == 2 ? 6 : 4) : (wc == 2 ? 4 : 0);
+}
+bool big1_split_ok(int wc, int nw, int wr) { return big1_rbd(wc, nw, wr) > 0; }
+
+int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, int wr, bool split, hipStream_t s) {
   FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && (wr == 8 || (wr == 4 && nw == 4)) && a0.cin % 8 == 0 &&
                 out_kind != OUT_DFL,
             "conv 1x1 big tile: bad configuration");
@@ -345,7 +389,17 @@ int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, int wr, hipStr
   const ConvArgs a = big_grid(a0, wc, nw, wr, grid);
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 1x1 big tile: grid too large");
   int rc;
-  if (nw == 8)
+  if (split) {
+    if (nw == 8)
+      rc = wc == 1 ? launch_big1_w<1, 8, 8, big1_rbd(1, 8, 8)>(a, out_kind, grid, s)
+                   : launch_big1_w<2, 8, 8, big1_rbd(2, 8, 8)>(a, out_kind, grid, s);
+    else if (wr == 8)
+      rc = wc == 1 ? fail(FCE_ERR_INVALID, "conv 1x1 big tile: no split rings for 4 waves x 128 couts, wc 1")
+                   : launch_big1_w<2, 4, 8, big1_rbd(2, 4, 8)>(a, out_kind, grid, s);
+    else
+      rc = wc == 1 ? launch_big1_w<1, 4, 4, big1_rbd(1, 4, 4)>(a, out_kind, grid, s)
+                   : launch_big1_w<2, 4, 4, big1_rbd(2, 4, 4)>(a, out_kind, grid, s);
+  } else if (nw == 8)
     rc = wc == 1 ? launch_big1_w<1, 8>(a, out_kind, grid, s) : launch_big1_w<2, 8>(a, out_kind, grid, s);
   else if (wr == 8)
     rc = wc == 1 ? launch_big1_w<1, 4>(a, out_kind, grid, s) : launch_big1_w<2, 4>(a, out_kind, grid, s);
