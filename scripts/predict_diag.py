@@ -59,8 +59,8 @@ def main():
     model = DetectionModel("yolo11n-fce.yaml")
     model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
     model.eval().to(dev)
-    for lanes, workers, cs, tiny in ((3, 8, False, False), (5, 8, False, False), (5, 4, False, False),
-                                     (5, 4, True, False), (6, 4, False, False), (5, 4, False, True)):
+    cfgs = [(5, 4, True, False), (6, 4, True, False), (6, 8, True, False), (7, 4, True, False), (8, 4, True, False)]
+    for lanes, workers, cs, tiny in cfgs + cfgs + [(6, 4, True, True), (8, 4, True, True)]:
         p = Predictor(model, B, 640, dev, lanes=lanes, workers=workers, copy_stream=cs)
         if tiny:  # 32x32 sources: no packing / PCIe cost to speak of
             batches = [[im[:32, :32].copy() for im in imgs]] * 2
