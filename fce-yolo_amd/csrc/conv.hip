@@ -2301,10 +2301,12 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
       for (int wm : {1, 2})
         if (n < cap && big3_ok(d.stride, wm, ab) && (wm == 1 || d.cout >= 128)) out[n++] = 0x800 | (wm << 4) | ((ab - 2) << 12);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && !no_gemm3())  // 0xC00
-    for (int nwc : {0, 1, 2})
-      for (int wcl = 0; wcl < 2; ++wcl)
-        if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles)
-          out[n++] = 0xC00 | (wcl << 4) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
+    for (int split : {0, 1})  // split rings (0x20): wc 2 only
+      for (int nwc : {0, 1, 2})
+        for (int wcl = split; wcl < 2; ++wcl)
+          if (n < cap && (((nwc == 2 ? 4 : 8) << wcl) >> 1) < cotiles &&
+              (!split || big1_split_ok(1 << wcl, nwc ? 4 : 8, nwc == 2 ? 4 : 8)))
+            out[n++] = 0xC00 | (wcl << 4) | (split << 5) | ((nwc > 0) << 6) | ((nwc == 2) << 7);
   // wide tile (opt-in, FCE_WIDE3=1: measured at parity or slower on every m/l shape): 0xA00 | cwl << 4
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0 && d.cin >= 64 && d.cout >= 64 && !det_box && wide3_on())
     for (int cwl = 0; cwl < 3; ++cwl)
@@ -2742,10 +2744,10 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   }
   if (kind == 12) {  // 256-wide-tile implicit-GEMM 3x3 kernel
     const int wc = 1 << ((tile >> 4) & 1), nw = (tile >> 6) & 1 ? 4 : 8, wr = (tile >> 7) & 1 ? 4 : 8;
-    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0x2F) == 0 && big1_ok(wc) &&
+    FCE_CHECK(d.k == 3 && fast && out_kind == OUT_F16 && d.up == 0 && (tile & 0x0F) == 0 && big1_ok(wc) &&
                   (wr == 8 || nw == 4),
               "conv: bad big-tile 3x3 (implicit GEMM) hint");
-    return launch_big3g(a, wc, nw, wr, d.stride, s);
+    return launch_big3g(a, wc, nw, wr, d.stride, (tile >> 5) & 1, s);
   }
   if (kind == 10) {  // wide-tile 3x3 kernel, per-K-step weight staging
     const int cw = 1 << ((tile >> 4) & 3);

@@ -304,6 +304,6 @@ int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
 bool big1_ok(int wc);
 bool big1_split_ok(int wc, int nw, int wr);
 int launch_big1(const ConvArgs& a, int out_kind, int wc, int nw, int wr, bool split, hipStream_t s);  // split: | 0x20
-int launch_big3g(const ConvArgs& a, int wc, int nw, int wr, int stride, hipStream_t s);
+int launch_big3g(const ConvArgs& a, int wc, int nw, int wr, int stride, bool split, hipStream_t s);
 
 }  // namespace fce

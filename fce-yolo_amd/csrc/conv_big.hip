@@ -410,12 +410,15 @@ int launch_big1(const ConvArgs& a0, int out_kind, int wc, int nw, int wr, bool s
 }
 
 template <int S, int NW, int WR>
-static int launch_big3g_s(const ConvArgs& a, int wc, dim3 grid, hipStream_t s) {
+static int launch_big3g_s(const ConvArgs& a, int wc, bool split, dim3 grid, hipStream_t s) {
+  if (split)  // split rings for the 3x3s: wc 2 only (256 / 128-cout blocks)
+    return wc == 2 ? launch_big_k<3, S, 2, NW, OUT_F16, WR, big1_rbd(2, NW, WR)>(a, grid, s)
+                   : fail(FCE_ERR_INVALID, "conv 3x3 big tile: split rings need wc 2");
   return wc == 1 ? launch_big_k<3, S, 1, NW, OUT_F16, WR>(a, grid, s)
                  : launch_big_k<3, S, 2, NW, OUT_F16, WR>(a, grid, s);
 }
 
-int launch_big3g(const ConvArgs& a0, int wc, int nw, int wr, int stride, hipStream_t s) {
+int launch_big3g(const ConvArgs& a0, int wc, int nw, int wr, int stride, bool split, hipStream_t s) {
   FCE_CHECK(big1_ok(wc) && (nw == 8 || nw == 4) && (wr == 8 || (wr == 4 && nw == 4)) && a0.cin % 32 == 0 &&
                 a0.up == 0 && (stride == 1 || stride == 2),
             "conv 3x3 big tile: bad configuration");
@@ -424,11 +427,13 @@ int launch_big3g(const ConvArgs& a0, int wc, int nw, int wr, int stride, hipStre
   FCE_CHECK(int64_t(grid.x) < (int64_t(1) << 31), "conv 3x3 big tile: grid too large");
   int rc;
   if (stride == 1)
-    rc = nw == 8 ? launch_big3g_s<1, 8, 8>(a, wc, grid, s)
-                 : wr == 8 ? launch_big3g_s<1, 4, 8>(a, wc, grid, s) : launch_big3g_s<1, 4, 4>(a, wc, grid, s);
+    rc = nw == 8 ? launch_big3g_s<1, 8, 8>(a, wc, split, grid, s)
+         : wr == 8 ? launch_big3g_s<1, 4, 8>(a, wc, split, grid, s)
+                   : launch_big3g_s<1, 4, 4>(a, wc, split, grid, s);
   else
-    rc = nw == 8 ? launch_big3g_s<2, 8, 8>(a, wc, grid, s)
-                 : wr == 8 ? launch_big3g_s<2, 4, 8>(a, wc, grid, s) : launch_big3g_s<2, 4, 4>(a, wc, grid, s);
+    rc = nw == 8 ? launch_big3g_s<2, 8, 8>(a, wc, split, grid, s)
+         : wr == 8 ? launch_big3g_s<2, 4, 8>(a, wc, split, grid, s)
+                   : launch_big3g_s<2, 4, 4>(a, wc, split, grid, s);
   if (rc != FCE_OK) return rc;
   return launch_status("conv_big_kernel");
 }
