@@ -14,7 +14,7 @@ A step = one global batch of B images per GPU through `dist.ShardedPredictor`: e
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
 with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
-default four batches are in flight per GPU on the n scale and three on the wider ones (--lanes, engine.Pipeline
+default four batches are in flight per GPU on the n scale with one GPU and three otherwise (--lanes, engine.Pipeline
 lanes): executors with their own arenas on their own streams, each running forward then NMS of every L-th batch, so one batch's
 latency-bound coarse layers and NMS share the CUs with the next batches' full-width layers; the gather
 runs on a side stream in batch order.  With four lanes the process asks HIP for 8 hardware queues
@@ -53,12 +53,16 @@ def launch_command(argv, env):
             "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
 
 
-def default_lanes(model: str, env) -> int:
-    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n scale (its four activation
-    arenas still fit the 256 MB MALL: 29.3-29.6k vs 28.7-28.8k images/s with 3) and 3 for the wider scales (l32
-    4 954 vs 4 573, m16-h8 1 625 vs 1 529 images/s with 4, profiles/r03y_*)."""
+def default_lanes(model: str, env, gpus: int = 1) -> int:
+    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n scale on one GPU (its four
+    activation arenas still fit the 256 MB MALL: 29.3-29.6k vs 28.7-28.8k images/s with 3) and 3 otherwise: the
+    wider scales (l32 4 954 vs 4 573, m16-h8 1 625 vs 1 529 images/s with 4, profiles/r03y_*) and every run with a
+    process group, where RCCL's streams share the hardware queues (one-rank RCCL path 27.8k with 3 lanes x 4 queues,
+    24.8-25.3k with 4 x 8, profiles/r03ad_*)."""
     if env.get("FCE_LANES"):
         return int(env["FCE_LANES"])
+    if gpus > 1 or int(env.get("WORLD_SIZE", "1") or 1) > 1 or env.get("FCE_DIST_FORCE") == "1":
+        return 3
     stem = Path(model).stem
     scale = stem[6:7] if stem.startswith("yolo11") else ""
     return 4 if scale == "n" else 3
@@ -71,8 +75,9 @@ def hw_queues_env(argv, env):
     pre = argparse.ArgumentParser(add_help=False)
     pre.add_argument("--model", default="yolo11n-fce.yaml")
     pre.add_argument("--lanes", type=int, default=None)
+    pre.add_argument("--gpus", type=int, default=1)
     a, _ = pre.parse_known_args(argv)
-    lanes = a.lanes if a.lanes is not None else default_lanes(a.model, env)
+    lanes = a.lanes if a.lanes is not None else default_lanes(a.model, env, a.gpus)
     have = int(env.get("GPU_MAX_HW_QUEUES", "4") or 4)
     return "8" if lanes >= 4 and have < 8 else None
 
@@ -154,7 +159,7 @@ def parse_args():
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
     a = ap.parse_args()
     if a.lanes is None:
-        a.lanes = default_lanes(a.model, os.environ)
+        a.lanes = default_lanes(a.model, os.environ, a.gpus)
     if a.graph < 0:
         a.graph = 1 if a.lanes > 1 else 0
     return a
