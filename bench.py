@@ -441,6 +441,10 @@ def main():
     if a.profile_json and rank == 0:
         Path(a.profile_json).write_text(json.dumps([list(p) for p in prof], indent=0))
     if rank == 0 and world == 1 and a.predict_steps > 0:
+        # the main line's lanes (executors, streams, arenas) are released first: the predict path brings its own
+        sp.close()
+        sp = eng = nms = None
+        torch.cuda.empty_cache()
         out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps, a.predict_lanes)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds, B)
@@ -453,7 +457,8 @@ def main():
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
-    sp.close()
+    if sp is not None:
+        sp.close()
 
 
 if __name__ == "__main__":
