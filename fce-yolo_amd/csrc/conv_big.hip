@@ -1,19 +1,21 @@
-// Big-tile implicit-GEMM convolution: the wide 1x1 and 3x3 convs of the m/l scales with 256-wide block tiles.
+// Big-tile implicit-GEMM convolution: the wide 1x1 and 3x3 convs of the m/l scales with 128-256-wide block tiles.
 // Replaces (reference, ultralytics/): nn/modules/conv.py:39-89 Conv.forward_fuse (BN folded by
 // utils/torch_utils.py:237-267) for 1x1 kernels -- the C2f / C3k / SPPF / C2PSA cv1 / cv2 / FFN pointwise convs, the
 // BiFPN realign convs (fce_block.py:24-38), nn.Upsample feeding a 1x1 conv -- and for 3x3 kernels with cin % 32 == 0
-// (the stride-2 downsampling convs and the wide bottleneck convs).  Variant codes 0xB00 | log2(wc) << 4 (1x1) and
-// 0xC00 | log2(wc) << 4 (3x3).
+// (the stride-2 downsampling convs and the wide bottleneck convs).  Variant codes 0xB00 (1x1) / 0xC00 (3x3) |
+// log2(wc) << 4 | split << 5 | (nw == 4) << 6 | (wr == 4) << 7.
 //
-// A block is 8 waves (512 threads): WC waves along the couts, each owning 8 cout tiles (128 couts), times 8 / WC
-// waves along the pixels, each owning 4 groups of 16 pixels (64 pixels): every wave runs 32 MFMAs per K-step from
-// 8 A + 4 B fragment reads (0.375 KiB of LDS reads per MFMA, against 0.5 for 64 x 64 wave tiles), and the block
-// stages 16 KiB of weights + 16 KiB of pixels per K-step.  The copies go global -> LDS by LDS-DMA
-// (global_load_lds) into a ring of K-step slots, issued 3-4 steps ahead: 96-128 KiB in flight per CU, which a
+// Geometry: NW waves per block (8: one block per CU; 4: two per CU, so one block's prologue and staged epilogue run
+// under the other's K loop), WC waves along the couts, each owning WR cout tiles (8: 128 couts; 4: 64, 4-wave blocks
+// only), times NW / WC waves along the pixels, each owning 4 groups of 16 pixels (64 pixels).  With WR = 8 every wave
+// runs 32 MFMAs per K-step from 8 A + 4 B fragment reads (0.375 KiB of LDS reads per MFMA, against 0.5 for 64 x 64
+// wave tiles).  The copies go global -> LDS by LDS-DMA (global_load_lds) into a ring of K-step slots issued RING - 1
+// steps ahead (5 slots for 8 waves x 256 couts, 4 for 8 x 128 and for 4 x 64-cout waves, 3 for 4 x 128-cout waves), or
+// (split) into two rings: the weights, L2 hits, 2 steps ahead, the pixels in a deeper ring 3-5 steps ahead.  A
 // register-staged version (one step ahead, 32 KiB in flight: measured ~2.6 TB/s effective, Little's law at HBM
-// latency) could not reach without spilling.  One raw s_barrier per step behind a counted vmcnt: a
-// __syncthreads() there makes hipcc wait vmcnt(0) first (a DMA is a pending LDS write), which drained the whole
-// ring every step.  The 1x1 form with WC = 2 uses a 5-slot ring (copies 4 steps ahead), WC = 1 a 4-slot ring.
+// latency) could not keep enough bytes in flight without spilling.  One raw s_barrier per step behind a counted
+// vmcnt: a __syncthreads() there makes hipcc wait vmcnt(0) first (a DMA is a pending LDS write), which drained the
+// whole ring every step.  The next step's fragments are read into a second register set while this step's MFMAs run.
 // 3x3 (implicit im2col): K-step j = (32-channel chunk j / 9, tap j % 9), the packed weights' chunk-major order;
 // every B piece of a step is the lane's pixel shifted by the tap, or the zero line outside the image, so stride 2
 // costs no more staging than stride 1.
