@@ -14,8 +14,8 @@ A step = one global batch of B images per GPU through `dist.ShardedPredictor`: e
 shard (reference ContiguousDistributedSampler rule) of resident synthetic input (torch.rand fp16, seeded
 per rank) runs the whole forward (a captured hipGraph replayed per lane; --graph 0 for direct launches) + the device NMS, and
 with N > 1 the packed detections of every rank are all-gathered (one RCCL collective per batch).  By
-default four batches are in flight per GPU on the n scale with one GPU and three otherwise (--lanes, engine.Pipeline
-lanes): executors with their own arenas on their own streams, each running forward then NMS of every L-th batch, so one batch's
+default four batches are in flight per GPU on the n and s scales with one GPU and three otherwise (--lanes,
+engine.Pipeline lanes): executors with their own arenas on their own streams, each running forward then NMS of every L-th batch, so one batch's
 latency-bound coarse layers and NMS share the CUs with the next batches' full-width layers; the gather
 runs on a side stream in batch order.  With four lanes the process asks HIP for 8 hardware queues
 (GPU_MAX_HW_QUEUES, set before torch is imported; HIP's default 4 is shared by the lanes, the side stream and
@@ -54,9 +54,10 @@ def launch_command(argv, env):
 
 
 def default_lanes(model: str, env, gpus: int = 1) -> int:
-    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n scale on one GPU (its four
-    activation arenas still fit the 256 MB MALL: 29.3-29.6k vs 28.7-28.8k images/s with 3) and 3 otherwise: the
-    wider scales (l32 4 954 vs 4 573, m16-h8 1 625 vs 1 529 images/s with 4, profiles/r03y_*) and every run with a
+    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n and s scales on one GPU
+    (n32 29.3-29.6k vs 28.7-28.8k images/s with 3, s32 16.0-16.1k vs 15.8k, profiles/r03w_*, r03ak_*) and 3
+    otherwise: the m / l scales, whose four arenas overflow the MALL (l32 4 954 vs 4 573, m16-h8 1 625 vs 1 529
+    images/s with 4, profiles/r03y_*), and every run with a
     process group, where RCCL's streams share the hardware queues (one-rank RCCL path 27.8k with 3 lanes x 4 queues,
     24.8-25.3k with 4 x 8, profiles/r03ad_*)."""
     if env.get("FCE_LANES"):
@@ -65,7 +66,7 @@ def default_lanes(model: str, env, gpus: int = 1) -> int:
         return 3
     stem = Path(model).stem
     scale = stem[6:7] if stem.startswith("yolo11") else ""
-    return 4 if scale == "n" else 3
+    return 4 if scale in ("n", "s") else 3
 
 
 def hw_queues_env(argv, env):
