@@ -1672,6 +1672,7 @@ __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
 // three accumulate with explicit fmaf in (ky, kx) order and pin the result before the fp16 conversion,
 // so hipcc cannot contract them differently.
 //   0 pixel-quad (dwconv_kernel<S,4>)   1 row-staged LDS (dwconv_rows_kernel)   2 lane-contiguous
+//   3 / 4 column runs of 2 / 4 outputs (dwconv_cols_kernel<S,PY>; runs of 8 measured slower on every n32 op)
 int dwconv_variants(int c, int w, int* out, int cap) {
   int n = 0;
   if (n < cap) out[n++] = 0;

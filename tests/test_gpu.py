@@ -692,6 +692,44 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     assert _rel(base, ref) <= 4e-3
 
 
+@pytest.mark.parametrize("c,stride,H,W,cpad", [
+    (64, 1, 80, 80, 0), (80, 1, 37, 45, 0), (80, 2, 41, 37, 0), (128, 1, 19, 23, 16), (256, 2, 20, 20, 0),
+    (24, 1, 11, 9, 8), (64, 2, 7, 5, 0),
+])
+def test_dwconv_every_variant_bitwise_and_parity(c, stride, H, W, cpad, device):
+    """Every depthwise 3x3 variant (pixel quads, row-staged LDS, lane-contiguous, column runs of 2 / 4) gives the
+    bit-identical result on channel-slice views, and matches the fp64 reference (Detect cls branch DWConv,
+    reference ultralytics/nn/modules/conv.py DWConv)."""
+    g = torch.Generator().manual_seed(c * 100 + H)
+    w = torch.randn(c, 1, 3, 3, generator=g) * (1.0 / 3)
+    b = torch.randn(c, generator=g) * 0.1
+    x = torch.randn(2, c, H, W, generator=g).half()
+    desc = N.ConvDesc(c, c, 3, stride, c, N.ACT_SILU, 0, 0, None, 0, 0)
+    wp = M.pack_conv(desc, w, device)
+    bd = b.float().to(device)
+    xbuf = torch.randn(2, H, W, c + cpad, generator=g).half().to(device)
+    xbuf[..., cpad:] = x.to(device).permute(0, 2, 3, 1)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    ref = torch.nn.functional.silu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, 1, groups=c))
+    xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, 2, c, H, W, c + cpad, cpad)
+    codes = (C.c_int * 128)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
+    assert set(codes[:nv]) >= {100, 102, 103, 104}
+    outs = {}
+    for code in [-1] + list(codes[:nv]):
+        y = torch.full((2, Ho, Wo, c + cpad), float("nan"), dtype=torch.float16, device=device)
+        yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, 2, c, Ho, Wo, c + cpad, cpad)
+        N.call("fce_conv2d_variant", C.byref(desc), C.byref(xt), wp.data_ptr(), bd.data_ptr(), None, C.byref(yt),
+               code, None)
+        yc = y.cpu()
+        assert torch.isnan(yc[..., :cpad]).all(), code
+        outs[code] = yc[..., cpad:].permute(0, 3, 1, 2)
+    base = outs[-1]
+    for code, y in outs.items():
+        assert torch.equal(y, base), (code, (y.float() - base.float()).abs().max().item())
+    assert _rel(base, ref) <= 4e-3
+
+
 @pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11s-bifpn.yaml", 2, 256),
                                              ("yolo11n-fce.yaml", 1, 640)])
 def test_every_op_variant_bitwise_in_model(cfg, batch, imgsz, device, monkeypatch):
