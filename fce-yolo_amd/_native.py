@@ -126,6 +126,7 @@ _SIGS = {
     "fce_letterbox": (_I, [_P, _I, _P, _I, _I, _I, _P]),
     "fce_scale_boxes": (_I, [_P, _P, _I, _I, _P, _P]),
     "fce_conv2d_variant": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _I, _P]),
+    "fce_conv2d_variant_dup": (_I, [_PCD, _PT, _P, _P, _PT, _PT, _I, _PT, _I, _P]),
     "fce_conv2d_detect": (_I, [_PCD, _PT, _P, _P, C.POINTER(DetectEpi), _P]),
     "fce_maxpool_chain": (_I, [_PT, _PT, _PT, _PT, _I, _P]),
     "fce_weighted_add": (_I, [_PT, _I, _P, _I, _I, _I, _PT, _P]),

@@ -108,6 +108,16 @@ int fce_conv2d_variant(const fce_conv_desc* d, const fce_tensor* x, const void* 
   FCE_CHECK(d && x && w && bias && y, "fce_conv2d_variant: null argument");
   FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream), variant);)
 }
+int fce_conv2d_variant_dup(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
+                           const fce_tensor* res, const fce_tensor* y, int variant, const fce_tensor* dup, int dup_lo,
+                           void* stream) {
+  FCE_CHECK(d && x && w && bias && y && dup, "fce_conv2d_variant_dup: null argument");
+  FCE_CHECK(d->k == 1 && d->groups == 1 && d->epilogue == FCE_EPI_STORE && dup->dtype == FCE_F16 &&
+                dup->layout == FCE_NHWC && dup_lo >= 0 && dup_lo % 8 == 0 && dup->c % 8 == 0 &&
+                dup_lo + dup->c <= d->cout && dup->n == y->n && dup->h == y->h && dup->w == y->w,
+            "fce_conv2d_variant_dup: the duplicate store needs a plain 1x1 conv and an aligned f16 view of y's size");
+  FCE_GUARD(return conv2d(*d, *x, w, bias, res, *y, S(stream), variant, dup, dup_lo);)
+}
 int fce_c3k2_supported(const fce_c3k2_desc* d) { return d && c3k2_fused_ok(*d) ? 1 : 0; }
 int fce_c3k2(const fce_c3k2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
   FCE_CHECK(d && x && y, "fce_c3k2: null argument");
@@ -680,10 +690,12 @@ int fce_net_add_conv_dup(fce_net* net, const fce_conv_desc* d, int in, int in_co
                 d && d->k == 1 && dup_lo + dup_c <= d->cout && net->bufs[dup].c == dup_c &&
                 net->bufs[dup].dtype == FCE_F16,
             "fce_net_add_conv_dup: bad duplicate-store buffer or channel range");
+  // every check before the op is added: a failed call leaves the op list unchanged
+  FCE_CHECK(valid_buf(net, out, false) && net->bufs[dup].shift == net->bufs[out].shift,
+            "fce_net_add_conv_dup: dup buffer size differs");
   const int st = fce_net_add_conv(net, d, in, in_coff, out, out_coff, res, res_coff, w, b);
   if (st) return st;
   OpDesc& op = net->ops.back();
-  FCE_CHECK(net->bufs[dup].shift == net->bufs[out].shift, "fce_net_add_conv_dup: dup buffer size differs");
   op.dup = dup;
   op.dup_lo = dup_lo;
   op.dup_c = dup_c;

@@ -6,10 +6,15 @@
 //   m = SiLU(m.cv2(h)) + b      3x3, c_mid -> c   (shortcut)
 //   y = SiLU(cv2([a | b | m]))  1x1, 3c -> cout
 //
-// in ONE kernel per 8 x 16 output tile (8 waves): x is read once (with a 2-pixel halo), t / h / m never leave
-// LDS, y is written once.  At the n scale (C3k2 at 160^2 and 80^2, 16-64 channels) the four separate
-// convs are HBM round trips of small tensors plus four launch tails; fused, the block is one read of x
-// and one write of y.
+// in ONE persistent kernel.  A block owns a contiguous run of TH x TW output tiles and keeps the four
+// convs' packed A fragments resident in LDS for its whole life (copied once); per tile
+//   stage 1: cv1 over the tile + 2-pixel halo, its B operands (x) loaded straight from HBM into registers
+//            while the PREVIOUS tile's stages 2-4 run (one read of x per tile, latency off the critical path),
+//   stage 2: m.cv1 over the tile + 1-pixel halo, from the t image in LDS,
+//   stage 3: m.cv2 + the residual b over the tile, into the m image in LDS,
+//   stage 4: cv2 over [a | b | m] from LDS, y to HBM.
+// t / h / m never leave LDS: the block is one read of x and one write of y (the four separate convs move
+// x, t twice, h twice, m twice and [a | b | m] through HBM, n32's L2 block alone ~390 MB against ~157 MB).
 //
 // Bitwise identical to the four unfused convs (conv_mfma_kernel and its variants): every stage walks
 // the same K-steps of the same packed A fragments (conv_pack: chunk-major for cin % 32 == 0, else
@@ -17,14 +22,19 @@
 // are the same fp16 values (intermediates rounded to fp16 exactly where the unfused path stores them,
 // zeros where it zero-pads), and the epilogue arithmetic is conv_epilogue's (bias, SiLU, residual add,
 // fpin before every fp16 conversion).
+#include <algorithm>
+
 #include "common.h"
 
 namespace fce {
 
-struct FStage {
-  const h8* w;      // packed A fragments (conv_pack layout)
-  const float* b;   // bias (BN folded)
-  int cin, cout, taps, fast, cpt, nsteps, nalloc, cotiles;
+static __device__ __attribute__((aligned(16))) _Float16 g_c3_zero[8];
+
+struct C3Stage {
+  const h8* w;     // packed A fragments in HBM (conv_pack layout: [cout tile][nalloc][64 lanes])
+  const float* b;  // bias (BN folded)
+  int cout, cotiles, nsteps, nalloc, fast, cpt, taps;
+  int wl;  // 16-byte offset of the stage's fragments in LDS: [cout tile][step][64 lanes]
 };
 
 struct C3k2Args {
@@ -32,176 +42,322 @@ struct C3k2Args {
   int xcs;
   _Float16* y;
   int ycs;
-  int N, H, W;
-  int c, c2;
-  FStage st[4];
-  int tiles_x, tiles_y;
-  int sx, sy, sh;  // LDS row strides (16-byte units) of the x, t|m and h images: odd, so 16 consecutive
-                   // positions meet 16 distinct 16-byte slots of a bank row (conflict-free B gathers)
-  int xh_off;      // 16-byte offset of the x / h image (h reuses x's space: x is dead after stage 1)
+  int N, H, W, c;
+  C3Stage st[4];
+  int TH, TW, tiles_x, tiles_y, ntiles;
+  int R2W, R2, R1W, R1, NC;  // cv1 region (tile + 2-pixel halo), m.cv1 region (+ 1 pixel), tile positions
+  int sT, sH, sM;            // LDS strides of the t, h, m images in 16-byte units (odd: conflict-free B reads)
+  int oT, oH, oM;            // their 16-byte offsets
+  int wtotal;                // 16-byte units of resident fragments
 };
 
-constexpr int FT_H = 8, FT_W = 16;
-constexpr int R2H = FT_H + 4, R2W = FT_W + 4;  // cv1 output region: tile + 2-pixel halo (two 3x3 convs)
-constexpr int R1H = FT_H + 2, R1W = FT_W + 2;  // m.cv1 output region: tile + 1-pixel halo
-constexpr int NR2 = R2H * R2W, NR1 = R1H * R1W, NCORE = FT_H * FT_W;
-
-constexpr int FNW = 4;  // waves per block (several blocks per CU overlap each other's stage barriers)
-
-// One stage: outputs at `npos` positions of a region OW wide, read from the LDS image `in` (row stride
-// sin, first channel chunk coff8) of a region IW wide (3x3: output (r, c) reads input (r + ky, c + kx);
-// 1x1: input (r + off, c + off)).  Wave w owns the 16-position fragments w, w + FNW (<= MAXF of them)
-// and all cout tiles; the K loop walks the packed steps with the A fragments of step s + 1 in flight
-// while step s's MFMAs run (one L2 latency per stage, not one per step and fragment).
-// epi(q, co0, v[4]) gets the 4 SiLU'd fp32 outputs of lane group grp.
-template <int MAXCT, int MAXF, typename Epi>
-__device__ __forceinline__ void fstage(const FStage& s, const h8* in, int sin, int coff8, int IW, int npos, int OW,
-                                       int off, Epi epi) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, grp = lane >> 4;
-  const int nfr = (npos + 15) >> 4;
-  if (wave >= nfr) return;  // wave-uniform
-  int base[MAXF];
-#pragma unroll
-  for (int i = 0; i < MAXF; ++i) {
-    const int q = min((wave + FNW * i) * 16 + col, npos - 1);
-    const int qr = q / OW, qc = q - qr * OW;
-    base[i] = s.taps == 9 ? qr * IW + qc : (qr + off) * IW + (qc + off);
-  }
-  f4 acc[MAXF][MAXCT];
-#pragma unroll
-  for (int i = 0; i < MAXF; ++i)
-#pragma unroll
-    for (int ct = 0; ct < MAXCT; ++ct) acc[i][ct] = f4{0.f, 0.f, 0.f, 0.f};
-  const h8* wl = s.w + lane;
-  h8 ac[MAXCT], an[MAXCT];
-#pragma unroll
-  for (int ct = 0; ct < MAXCT; ++ct)
-    if (ct < s.cotiles) ac[ct] = wl[(size_t(ct) * s.nalloc) * 64];
-  for (int st = 0; st < s.nsteps; ++st) {
-    const int sn = st + 1 < s.nsteps ? st + 1 : st;
-#pragma unroll
-    for (int ct = 0; ct < MAXCT; ++ct)
-      if (ct < s.cotiles) an[ct] = wl[(size_t(ct) * s.nalloc + sn) * 64];
-    int tap, c8;
-    bool ok;
-    if (s.fast) {  // step = 32-channel chunk * taps + tap
-      const int ch = st / s.taps;
-      tap = st - ch * s.taps;
-      c8 = ch * 4 + grp;
-      ok = true;
-    } else {  // 8-channel chunk c = 4 step + lane group, tap-major
-      const int cc = st * 4 + grp;
-      tap = cc / s.cpt;
-      c8 = cc - tap * s.cpt;
-      ok = tap < s.taps;
-    }
-    const int ky = (tap * 11) >> 5, kx = tap - ky * 3;  // tap / 3 for tap < 9
-    const int toff = s.taps == 9 ? ky * IW + kx : 0;
-#pragma unroll
-    for (int i = 0; i < MAXF; ++i) {
-      if (wave + FNW * i >= nfr) break;
-      const h8 bf = ok ? in[(base[i] + toff) * sin + coff8 + c8] : h8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int ct = 0; ct < MAXCT; ++ct)
-        if (ct < s.cotiles) acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[ct], bf, acc[i][ct], 0, 0, 0);
-    }
-#pragma unroll
-    for (int ct = 0; ct < MAXCT; ++ct) ac[ct] = an[ct];
-  }
-#pragma unroll
-  for (int i = 0; i < MAXF; ++i) {
-    const int qq = (wave + FNW * i) * 16 + col;
-    if (wave + FNW * i >= nfr || qq >= npos) continue;
-#pragma unroll
-    for (int ct = 0; ct < MAXCT; ++ct) {
-      const int co0 = ct * 16 + grp * 4;
-      if (ct >= s.cotiles || co0 >= s.cout) continue;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float t = acc[i][ct][j] + s.b[co0 + j];
-        v[j] = silu(t);
-      }
-      epi(qq, co0, v);
-    }
-  }
-}
-
-__device__ __forceinline__ h4 to_h4(const float (&v)[4]) {
+__device__ __forceinline__ h4 c3_h4(const float (&v)[4]) {
   return h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
 }
 
-template <int MAXCT>
-__global__ __launch_bounds__(FNW * 64) void c3k2_fused_kernel(C3k2Args a) {
-  extern __shared__ __attribute__((aligned(16))) h8 fsm[];
-  h8* Y = fsm;              // [NR2][sy]: a | b | m (m at the core positions only)
-  h8* XH = fsm + a.xh_off;  // [NR2][sx] x, then [NR1][sh] h
-  int t = blockIdx.x;
+// The wave's MF 16-position fragments f0, f0 + NW, ... (nf of them valid) x cout tiles [c0, c0 + MCT) of one
+// stage, every K-step; A from the stage's LDS fragments, B from bl(i, step) (base[] precomputed by the caller),
+// the next step's operands read while this step's MFMAs run.  epi(i, ct, acc) per valid (fragment, tile).
+template <int MF, int MCT, typename BL, typename EPI>
+__device__ __forceinline__ void c3_mma(const h8* wl, int ns, int cot, int c0, int nf, BL bl, EPI epi) {
+  f4 acc[MF][MCT];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int ct = 0; ct < MCT; ++ct) acc[i][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 av[MCT], bv[MF];
+#pragma unroll
+  for (int ct = 0; ct < MCT; ++ct)
+    if (c0 + ct < cot) av[ct] = wl[((c0 + ct) * ns) * 64];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+    if (i < nf) bv[i] = bl(i, 0);
+  for (int st = 0; st < ns; ++st) {
+    h8 an[MCT], bn[MF];
+    const int sn = st + 1 < ns ? st + 1 : st;
+#pragma unroll
+    for (int ct = 0; ct < MCT; ++ct)
+      if (c0 + ct < cot) an[ct] = wl[((c0 + ct) * ns + sn) * 64];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+      if (i < nf) bn[i] = bl(i, sn);
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int ct = 0; ct < MCT; ++ct)
+        if (i < nf && c0 + ct < cot) acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[ct], bv[i], acc[i][ct], 0, 0, 0);
+#pragma unroll
+    for (int ct = 0; ct < MCT; ++ct) av[ct] = an[ct];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) bv[i] = bn[i];
+  }
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int ct = 0; ct < MCT; ++ct)
+      if (i < nf && c0 + ct < cot) epi(i, c0 + ct, acc[i][ct]);
+}
+
+// SiLU(acc + bias) of lane group grp's 4 couts of tile ct
+__device__ __forceinline__ void c3_act(const C3Stage& s, int ct, int grp, const f4& acc, float (&v)[4]) {
+  const int co0 = ct * 16 + grp * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = silu(acc[j] + s.b[co0 + j]);
+}
+
+// decode tile t of the block's run -> image n, output origin (y0, x0)
+__device__ __forceinline__ void c3_tile(const C3k2Args& a, int t, int& n, int& y0, int& x0) {
   const int tx = t % a.tiles_x;
   t /= a.tiles_x;
   const int ty = t % a.tiles_y;
-  const int n = t / a.tiles_y;
-  const int y0 = ty * FT_H, x0 = tx * FT_W;
-  const int c8 = a.c / 8;
+  n = t / a.tiles_y;
+  y0 = ty * a.TH;
+  x0 = tx * a.TW;
+}
 
-  // stage 0: x over the 2-pixel-halo region, zeros outside the image
-  {
-    const int cpt = a.st[0].cpt, np = NR2 * cpt;
-    for (int e = threadIdx.x; e < np; e += FNW * 64) {
-      const int p = e / cpt, cc = e - p * cpt;
-      const int r = p / R2W, q = p - r * R2W;
-      const int iy = y0 - 2 + r, ix = x0 - 2 + q;
-      h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-        v = *reinterpret_cast<const h8*>(a.x + nhwc_off(n, iy, ix, a.H, a.W, a.xcs) + cc * 8);
-      XH[p * a.sx + cc] = v;
+// stage-1 B operands of tile t: x at the cv1 region's positions (zero line outside the image)
+template <int NW, int MF1, int NS1>
+__device__ __forceinline__ void c3_load_x(const C3k2Args& a, int t, h8 (&xb)[MF1][NS1]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, grp = lane >> 4;
+  int n, y0, x0;
+  c3_tile(a, t, n, y0, x0);
+  const _Float16* zl = g_c3_zero;
+#pragma unroll
+  for (int i = 0; i < MF1; ++i) {
+    const int q = (wave + NW * i) * 16 + col;
+    const int r = q / a.R2W, cc = q - r * a.R2W;
+    const int iy = y0 - 2 + r, ix = x0 - 2 + cc;
+    const bool in = q < a.R2 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    const _Float16* src = a.x + (in ? nhwc_off(n, iy, ix, a.H, a.W, a.xcs) + grp * 8 : 0);
+#pragma unroll
+    for (int s = 0; s < NS1; ++s) xb[i][s] = *reinterpret_cast<const h8*>(in ? src + s * 32 : zl);
+  }
+}
+
+template <int NW, int MF1, int NS1>
+__global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
+  extern __shared__ __attribute__((aligned(16))) h8 sm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, grp = lane >> 4;
+  const int G = gridDim.x, bi = blockIdx.x;
+  const int t_begin = int(int64_t(bi) * a.ntiles / G), t_end = int(int64_t(bi + 1) * a.ntiles / G);
+  if (t_begin >= t_end) return;  // block-uniform
+
+  h8 xb[MF1][NS1];
+  c3_load_x<NW, MF1, NS1>(a, t_begin, xb);
+  // the four convs' fragments -> LDS, once per block (batches of 4 loads in flight per thread)
+#pragma unroll 1
+  for (int s = 0; s < 4; ++s) {
+    const C3Stage& S = a.st[s];
+    const int nfr = S.cotiles * S.nsteps * 64;
+    for (int e0 = int(threadIdx.x); e0 < nfr; e0 += 4 * NW * 64) {
+      h8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * NW * 64;
+        const int k = e >> 6, ct = k / S.nsteps, stp = k - ct * S.nsteps;
+        if (e < nfr) v[u] = S.w[(size_t(ct) * S.nalloc + stp) * 64 + (e & 63)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * NW * 64;
+        if (e < nfr) sm[S.wl + e] = v[u];
+      }
     }
   }
   __syncthreads();
-  // stage 1: t = cv1(x) over the region; 0 outside the image (the 3x3 convs' zero padding of b)
-  fstage<MAXCT, (NR2 + 16 * FNW - 1) / (16 * FNW)>(a.st[0], XH, a.sx, 0, R2W, NR2, R2W, 0, [&](int q, int co0, float (&v)[4]) {
-    const int r = q / R2W, cq = q - r * R2W;
-    const int iy = y0 - 2 + r, ix = x0 - 2 + cq;
-    const bool in = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    h4 o = to_h4(v);
-    if (!in) o = h4{0, 0, 0, 0};
-    *reinterpret_cast<h4*>(reinterpret_cast<_Float16*>(Y + q * a.sy) + co0) = o;
-  });
-  __syncthreads();
-  // stage 2: h = m.cv1(b) over the 1-pixel-halo region; 0 outside the image
-  fstage<MAXCT, (NR2 + 16 * FNW - 1) / (16 * FNW)>(a.st[1], Y, a.sy, c8, R2W, NR1, R1W, 0, [&](int q, int co0, float (&v)[4]) {
-    const int r = q / R1W, cq = q - r * R1W;
-    const int iy = y0 - 1 + r, ix = x0 - 1 + cq;
-    const bool in = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    h4 o = to_h4(v);
-    if (!in) o = h4{0, 0, 0, 0};
-    *reinterpret_cast<h4*>(reinterpret_cast<_Float16*>(XH + q * a.sh) + co0) = o;
-  });
-  __syncthreads();
-  // stage 3: m = m.cv2(h) + b over the tile, into t's third channel block
-  fstage<MAXCT, (NR2 + 16 * FNW - 1) / (16 * FNW)>(a.st[2], XH, a.sh, 0, R1W, NCORE, FT_W, 0, [&](int q, int co0, float (&v)[4]) {
-    const int r = q / FT_W, cq = q - r * FT_W;
-    _Float16* yp = reinterpret_cast<_Float16*>(Y + ((r + 2) * R2W + cq + 2) * a.sy);
-    const h4 rv = *reinterpret_cast<const h4*>(yp + a.c + co0);
+
+  const int c8 = a.c / 8;
+  const int nfr1 = (a.R2 + 15) >> 4, nfr2 = (a.R1 + 15) >> 4, nfr4 = (a.NC + 15) >> 4;
+  _Float16* T = reinterpret_cast<_Float16*>(sm + a.oT);
+  _Float16* Hh = reinterpret_cast<_Float16*>(sm + a.oH);
+  _Float16* Mm = reinterpret_cast<_Float16*>(sm + a.oM);
+  constexpr int MF = 4, MCT = 4;
+
+  for (int t = t_begin; t < t_end; ++t) {
+    int n, y0, x0;
+    c3_tile(a, t, n, y0, x0);
+    // ---------------- stage 1: t = cv1(x) over the cv1 region (B operands already in registers)
+    {
+      const C3Stage& S = a.st[0];
+      const h8* wl = sm + S.wl + lane;
+      const int nf = wave < nfr1 ? min(MF1, (nfr1 - wave + NW - 1) / NW) : 0;
+      if (nf > 0) {
+        for (int c0 = 0; c0 < S.cotiles; c0 += MCT) {
+          f4 acc[MF1][MCT];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
-    *reinterpret_cast<h4*>(yp + 2 * a.c + co0) = to_h4(v);
-  });
-  __syncthreads();
-  // stage 4: y = cv2([a | b | m]) over the tile, to global
-  fstage<MAXCT, (NR2 + 16 * FNW - 1) / (16 * FNW)>(a.st[3], Y, a.sy, 0, R2W, NCORE, FT_W, 2, [&](int q, int co0, float (&v)[4]) {
-    const int r = q / FT_W, cq = q - r * FT_W;
-    const int iy = y0 + r, ix = x0 + cq;
-    if (iy < a.H && ix < a.W)
-      *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + co0) = to_h4(v);
-  });
+          for (int i = 0; i < MF1; ++i)
+#pragma unroll
+            for (int ct = 0; ct < MCT; ++ct) acc[i][ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NS1; ++s) {
+            h8 av[MCT];
+#pragma unroll
+            for (int ct = 0; ct < MCT; ++ct)
+              if (c0 + ct < S.cotiles) av[ct] = wl[((c0 + ct) * NS1 + s) * 64];
+#pragma unroll
+            for (int i = 0; i < MF1; ++i)
+#pragma unroll
+              for (int ct = 0; ct < MCT; ++ct)
+                if (i < nf && c0 + ct < S.cotiles)
+                  acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[ct], xb[i][s], acc[i][ct], 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < MF1; ++i) {
+            const int q = (wave + NW * i) * 16 + col;
+            if (i >= nf || q >= a.R2) continue;
+            const int r = q / a.R2W, cq = q - r * a.R2W;
+            const int iy = y0 - 2 + r, ix = x0 - 2 + cq;
+            const bool in = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+#pragma unroll
+            for (int ct = 0; ct < MCT; ++ct) {
+              if (c0 + ct >= S.cotiles) continue;
+              float v[4];
+              c3_act(S, c0 + ct, grp, acc[i][ct], v);
+              h4 o = c3_h4(v);
+              if (!in) o = h4{0, 0, 0, 0};  // the 3x3 convs' zero padding of b
+              *reinterpret_cast<h4*>(T + (q * a.sT) * 8 + (c0 + ct) * 16 + grp * 4) = o;
+            }
+          }
+        }
+      }
+    }
+    if (t + 1 < t_end) c3_load_x<NW, MF1, NS1>(a, t + 1, xb);  // in flight during stages 2-4
+    __syncthreads();
+    // ---------------- stage 2: h = m.cv1(b) over the m.cv1 region (3x3 from the t image)
+    {
+      const C3Stage& S = a.st[1];
+      const h8* wl = sm + S.wl + lane;
+      const h8* Tin = sm + a.oT;
+      for (int f0 = wave; f0 < nfr2; f0 += NW * MF) {
+        const int nf = min(MF, (nfr2 - f0 + NW - 1) / NW);
+        int pb[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int q = min((f0 + NW * i) * 16 + col, a.R1 - 1);
+          const int r = q / a.R1W, cq = q - r * a.R1W;
+          pb[i] = r * a.R2W + cq;  // tap (0, 0) of output (r, cq): R2 position (r + 1 - 1, cq + 1 - 1)
+        }
+        auto bl = [&](int i, int st) -> h8 {
+          int tap, cc;
+          bool ok = true;
+          if (S.fast) {
+            const int ch = st / 9;
+            tap = st - ch * 9;
+            cc = ch * 4 + grp;
+          } else {
+            const int k = st * 4 + grp;
+            tap = k / S.cpt;
+            cc = k - tap * S.cpt;
+            ok = tap < 9;
+          }
+          const int ky = (tap * 11) >> 5, kx = tap - ky * 3;
+          return ok ? Tin[(pb[i] + ky * a.R2W + kx) * a.sT + c8 + cc] : h8{0, 0, 0, 0, 0, 0, 0, 0};
+        };
+        auto epi = [&](int i, int ct, const f4& acc) {
+          const int q = (f0 + NW * i) * 16 + col;
+          if (q >= a.R1) return;
+          const int r = q / a.R1W, cq = q - r * a.R1W;
+          const int iy = y0 - 1 + r, ix = x0 - 1 + cq;
+          float v[4];
+          c3_act(S, ct, grp, acc, v);
+          h4 o = c3_h4(v);
+          if (!(iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)) o = h4{0, 0, 0, 0};
+          *reinterpret_cast<h4*>(Hh + (q * a.sH) * 8 + ct * 16 + grp * 4) = o;
+        };
+        for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
+      }
+    }
+    __syncthreads();
+    // ---------------- stage 3: m = m.cv2(h) + b over the tile (3x3 from the h image)
+    {
+      const C3Stage& S = a.st[2];
+      const h8* wl = sm + S.wl + lane;
+      const h8* Hin = sm + a.oH;
+      for (int f0 = wave; f0 < nfr4; f0 += NW * MF) {
+        const int nf = min(MF, (nfr4 - f0 + NW - 1) / NW);
+        int pb[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int q = min((f0 + NW * i) * 16 + col, a.NC - 1);
+          const int r = q / a.TW, cq = q - r * a.TW;
+          pb[i] = r * a.R1W + cq;
+        }
+        auto bl = [&](int i, int st) -> h8 {
+          int tap, cc;
+          bool ok = true;
+          if (S.fast) {
+            const int ch = st / 9;
+            tap = st - ch * 9;
+            cc = ch * 4 + grp;
+          } else {
+            const int k = st * 4 + grp;
+            tap = k / S.cpt;
+            cc = k - tap * S.cpt;
+            ok = tap < 9;
+          }
+          const int ky = (tap * 11) >> 5, kx = tap - ky * 3;
+          return ok ? Hin[(pb[i] + ky * a.R1W + kx) * a.sH + cc] : h8{0, 0, 0, 0, 0, 0, 0, 0};
+        };
+        auto epi = [&](int i, int ct, const f4& acc) {
+          const int q = (f0 + NW * i) * 16 + col;
+          if (q >= a.NC) return;
+          const int r = q / a.TW, cq = q - r * a.TW;
+          float v[4];
+          c3_act(S, ct, grp, acc, v);
+          const int co0 = ct * 16 + grp * 4;
+          const h4 rv = *reinterpret_cast<const h4*>(T + (((r + 2) * a.R2W + cq + 2) * a.sT) * 8 + a.c + co0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
+          *reinterpret_cast<h4*>(Mm + (q * a.sM) * 8 + co0) = c3_h4(v);
+        };
+        for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
+      }
+    }
+    __syncthreads();
+    // ---------------- stage 4: y = cv2([a | b | m]) over the tile, to HBM
+    {
+      const C3Stage& S = a.st[3];
+      const h8* wl = sm + S.wl + lane;
+      const h8* Tin = sm + a.oT;
+      const h8* Min = sm + a.oM;
+      const int c2 = 2 * c8, c3 = 3 * c8;
+      for (int f0 = wave; f0 < nfr4; f0 += NW * MF) {
+        const int nf = min(MF, (nfr4 - f0 + NW - 1) / NW);
+        int pt[MF], pm[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int q = min((f0 + NW * i) * 16 + col, a.NC - 1);
+          const int r = q / a.TW, cq = q - r * a.TW;
+          pt[i] = ((r + 2) * a.R2W + cq + 2) * a.sT;
+          pm[i] = q * a.sM - c2;
+        }
+        auto bl = [&](int i, int st) -> h8 {
+          const int cc = st * 4 + grp;  // 1x1 (either K order): the 8-channel chunk of [a | b | m]
+          if (cc >= c3) return h8{0, 0, 0, 0, 0, 0, 0, 0};
+          return cc < c2 ? Tin[pt[i] + cc] : Min[pm[i] + cc];
+        };
+        auto epi = [&](int i, int ct, const f4& acc) {
+          const int q = (f0 + NW * i) * 16 + col;
+          if (q >= a.NC) return;
+          const int r = q / a.TW, cq = q - r * a.TW;
+          const int iy = y0 + r, ix = x0 + cq;
+          if (iy >= a.H || ix >= a.W) return;
+          float v[4];
+          c3_act(S, ct, grp, acc, v);
+          *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + ct * 16 + grp * 4) = c3_h4(v);
+        };
+        for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
+      }
+    }
+    __syncthreads();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
+  }
 }
 
-static FStage make_stage(const fce_conv_desc& d, const void* w, const float* b) {
-  FStage s;
+// ============================================================================ host
+static C3Stage make_stage(const fce_conv_desc& d, const void* w, const float* b) {
+  C3Stage s{};
   s.w = static_cast<const h8*>(w);
   s.b = b;
-  s.cin = d.cin;
   s.cout = d.cout;
   s.taps = d.k * d.k;
   s.fast = d.cin % 32 == 0;
@@ -213,19 +369,88 @@ static FStage make_stage(const fce_conv_desc& d, const void* w, const float* b) 
   return s;
 }
 
-static size_t c3k2_lds_bytes(int cin, int c, int cm, int* sx, int* sy, int* sh, int* xh_off) {
-  *sx = (cin / 8) | 1;
-  *sy = (3 * c / 8) | 1;
-  *sh = (cm / 8) | 1;
-  *xh_off = NR2 * *sy;
-  const int xh = std::max(NR2 * *sx, NR1 * *sh);
-  return size_t(*xh_off + xh) * 16;
+struct C3Plan {
+  int TH, TW, NW, MF1;
+  size_t lds;
+};
+
+static int c3_weights16(const fce_c3k2_desc& d, C3Stage (&st)[4]) {
+  const fce_conv_desc c1{d.cin, 2 * d.c, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+  const fce_conv_desc m1{d.c, d.c_mid, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+  const fce_conv_desc m2{d.c_mid, d.c, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+  const fce_conv_desc c2{3 * d.c, d.cout, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+  const fce_conv_desc* cd[4] = {&c1, &m1, &m2, &c2};
+  int off = 0;
+  for (int i = 0; i < 4; ++i) {
+    st[i] = make_stage(*cd[i], d.w[i], d.b[i]);
+    st[i].wl = off;
+    off += st[i].cotiles * st[i].nsteps * 64;
+  }
+  return off;
+}
+
+// LDS image of a (TH, TW) tile: t = [a | b] over the cv1 region, h over the m.cv1 region, m over the tile
+static size_t c3_lds(const fce_c3k2_desc& d, int w16, int TH, int TW) {
+  const int R2 = (TH + 4) * (TW + 4), R1 = (TH + 2) * (TW + 2), NC = TH * TW;
+  const int sT = (2 * d.c / 8) | 1, sH = (d.c_mid / 8) | 1, sM = (d.c / 8) | 1;
+  return size_t(w16 + R2 * sT + R1 * sH + NC * sM) * 16;
+}
+
+// tile / waves for a map: 4 waves with two blocks per CU on wide maps, 8 waves and one block per CU
+// (the larger weight sets) otherwise; FCE_C3K2_TILE="TH,TW,NW" overrides (tuning)
+static bool c3_plan(const fce_c3k2_desc& d, int H, int W, int w16, C3Plan* p) {
+  const char* env = getenv("FCE_C3K2_TILE");  // read per plan: tests switch it within one process
+  int cand[6][3] = {{8, 16, 4}, {4, 40, 8}, {4, 32, 8}, {4, 16, 8}, {2, 40, 8}, {2, 16, 8}};
+  int nc = 6, first = W >= 128 ? 0 : 1;
+  if (env && *env) {
+    int th, tw, nw;
+    if (sscanf(env, "%d,%d,%d", &th, &tw, &nw) == 3 && th > 0 && tw > 0 && (nw == 4 || nw == 8)) {
+      cand[0][0] = th;
+      cand[0][1] = tw;
+      cand[0][2] = nw;
+      nc = 1;
+      first = 0;
+    }
+  }
+  for (int i = first; i < nc; ++i) {
+    const int TH = std::min(cand[i][0], H), TW = std::min(cand[i][1], W), NW = cand[i][2];
+    const int nfr1 = ((TH + 4) * (TW + 4) + 15) / 16;
+    const int mf1 = (nfr1 + NW - 1) / NW;
+    const size_t lds = c3_lds(d, w16, TH, TW);
+    if (mf1 > 4 || lds > 160 * 1024) continue;
+    *p = C3Plan{TH, TW, NW, mf1 <= 2 ? 2 : 4, lds};
+    return true;
+  }
+  return false;
 }
 
 bool c3k2_fused_ok(const fce_c3k2_desc& d) {
-  int sx, sy, sh, xo;
-  return d.cin % 8 == 0 && d.c % 8 == 0 && d.c_mid % 8 == 0 && d.cout % 4 == 0 && 2 * d.c <= 128 &&
-         d.c_mid <= 128 && d.c <= 128 && d.cout <= 128 && c3k2_lds_bytes(d.cin, d.c, d.c_mid, &sx, &sy, &sh, &xo) <= 160 * 1024;
+  if (!(d.cin % 32 == 0 && d.cin <= 64 && d.c % 16 == 0 && d.c_mid % 16 == 0 && d.cout % 16 == 0 && 2 * d.c <= 128 &&
+        d.c_mid <= 128 && d.cout <= 128))
+    return false;
+  C3Stage st[4];
+  const int w16 = c3_weights16(d, st);
+  C3Plan p;  // the candidates end with (2, 16): if some tile fits a 16-wide map, one fits every map
+  return c3_plan(d, 16, 16, w16, &p);
+}
+
+template <int NW, int MF1, int NS1>
+static int c3_launch(const C3k2Args& a, const C3Plan& p, hipStream_t s) {
+  auto k = c3k2_fused_kernel<NW, MF1, NS1>;
+  static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!big && p.lds > 64 * 1024) return fail(FCE_ERR_HIP, "c3k2 fused: cannot opt in to >64 KiB LDS");
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, NW * 64, p.lds) != hipSuccess || occ < 1) occ = 1;
+  const int grid = int(std::min<int64_t>(a.ntiles, int64_t(cus) * occ));
+  FCE_LAUNCH(k, dim3(unsigned(grid)), dim3(NW * 64), p.lds, s, a);
+  return launch_status("c3k2_fused_kernel");
 }
 
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s) {
@@ -236,11 +461,10 @@ int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y,
   FCE_CHECK(x.cstride % 8 == 0 && x.coff % 8 == 0 && y.cstride % 4 == 0 && y.coff % 4 == 0,
             "c3k2 fused: aligned channel slices");
   for (int i = 0; i < 4; ++i) FCE_CHECK(d.w[i] && d.b[i], "c3k2 fused: null weights");
-  const fce_conv_desc c1{d.cin, 2 * d.c, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
-  const fce_conv_desc m1{d.c, d.c_mid, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
-  const fce_conv_desc m2{d.c_mid, d.c, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
-  const fce_conv_desc c2{3 * d.c, d.cout, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
-  C3k2Args a;
+  C3k2Args a{};
+  const int w16 = c3_weights16(d, a.st);
+  C3Plan p;
+  FCE_CHECK(c3_plan(d, x.h, x.w, w16, &p), "c3k2 fused: no tile fits the LDS");
   a.x = static_cast<const _Float16*>(x.data) + x.coff;
   a.xcs = x.cstride;
   a.y = static_cast<_Float16*>(y.data) + y.coff;
@@ -249,31 +473,43 @@ int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y,
   a.H = x.h;
   a.W = x.w;
   a.c = d.c;
-  a.c2 = d.cout;
-  a.st[0] = make_stage(c1, d.w[0], d.b[0]);
-  a.st[1] = make_stage(m1, d.w[1], d.b[1]);
-  a.st[2] = make_stage(m2, d.w[2], d.b[2]);
-  a.st[3] = make_stage(c2, d.w[3], d.b[3]);
-  a.tiles_x = (x.w + FT_W - 1) / FT_W;
-  a.tiles_y = (x.h + FT_H - 1) / FT_H;
-  const size_t lds = c3k2_lds_bytes(d.cin, d.c, d.c_mid, &a.sx, &a.sy, &a.sh, &a.xh_off);
-  const int64_t blocks = int64_t(a.tiles_x) * a.tiles_y * x.n;
-  if (blocks == 0) return FCE_OK;
-  FCE_CHECK(blocks < (int64_t(1) << 31), "c3k2 fused: grid too large");
-  int maxct = 0;
-  for (const FStage& st : a.st) maxct = std::max(maxct, st.cotiles);
-  if (maxct <= 4) {  // fewer accumulator / fragment registers: more blocks per CU
-    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k2_fused_kernel<4>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    if (!big && lds > 64 * 1024) return fail(FCE_ERR_HIP, "c3k2 fused: cannot opt in to >64 KiB LDS");
-    FCE_LAUNCH(c3k2_fused_kernel<4>, dim3(unsigned(blocks)), dim3(FNW * 64), lds, s, a);
-  } else {
-    static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k2_fused_kernel<8>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    if (!big && lds > 64 * 1024) return fail(FCE_ERR_HIP, "c3k2 fused: cannot opt in to >64 KiB LDS");
-    FCE_LAUNCH(c3k2_fused_kernel<8>, dim3(unsigned(blocks)), dim3(FNW * 64), lds, s, a);
+  a.TH = p.TH;
+  a.TW = p.TW;
+  a.tiles_x = (x.w + p.TW - 1) / p.TW;
+  a.tiles_y = (x.h + p.TH - 1) / p.TH;
+  const int64_t tiles = int64_t(a.tiles_x) * a.tiles_y * x.n;
+  if (tiles == 0) return FCE_OK;
+  FCE_CHECK(tiles < (int64_t(1) << 30), "c3k2 fused: grid too large");
+  a.ntiles = int(tiles);
+  a.R2W = p.TW + 4;
+  a.R2 = (p.TH + 4) * a.R2W;
+  a.R1W = p.TW + 2;
+  a.R1 = (p.TH + 2) * a.R1W;
+  a.NC = p.TH * p.TW;
+  a.sT = (2 * d.c / 8) | 1;
+  a.sH = (d.c_mid / 8) | 1;
+  a.sM = (d.c / 8) | 1;
+  a.wtotal = w16;
+  a.oT = w16;
+  a.oH = a.oT + a.R2 * a.sT;
+  a.oM = a.oH + a.R1 * a.sH;
+  const int ns1 = d.cin / 32;
+  // host-side shape checks of what the kernel's indexing assumes
+  FCE_CHECK(a.st[0].nsteps == ns1 && a.st[0].fast, "c3k2 fused: cv1 K-steps");
+  FCE_CHECK((a.R2 + 15) / 16 <= p.NW * p.MF1, "c3k2 fused: cv1 region exceeds the wave fragments");
+  FCE_CHECK(size_t(a.oM + a.NC * a.sM) * 16 == p.lds, "c3k2 fused: LDS layout");
+#define C3L(NW_, MF_)                                                      \
+  do {                                                                     \
+    if (ns1 == 1) return c3_launch<NW_, MF_, 1>(a, p, s);                  \
+    return c3_launch<NW_, MF_, 2>(a, p, s);                                \
+  } while (0)
+  if (p.NW == 4) {
+    if (p.MF1 == 2) C3L(4, 2);
+    C3L(4, 4);
   }
-  return launch_status("c3k2_fused_kernel");
+  if (p.MF1 == 2) C3L(8, 2);
+  C3L(8, 4);
+#undef C3L
 }
 
 }  // namespace fce

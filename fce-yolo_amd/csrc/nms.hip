@@ -1105,7 +1105,10 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
   // FCE_NMS_V2=1: the multi-workgroup path (opt-in: measured slower on the bench batch)
   const char* v2e = getenv("FCE_NMS_V2");
   const bool v1 = !(v2e && atoi(v2e) != 0);
-  if (!multi && A > 0 && max_det <= KEPT_CAP && !v1 && stop == 0)
+  // V2 only where its greedy workgroup's LDS (candidate flags + 24 B per kept box) fits 64 KiB; every other
+  // configuration (multi_label, max_det > KEPT_CAP, a large max_det) takes the one-workgroup kernel
+  const bool v2_lds = size_t((std::min(A, max_nms) + 15) & ~15) + size_t(max_det) * 24 <= 64 * 1024;
+  if (!multi && A > 0 && max_det <= KEPT_CAP && !v1 && stop == 0 && v2_lds)
     return nms2(pred, best, n, nc, A, conf, iou, max_det, max_nms, max_wh, static_cast<char*>(ws), per, dets, keep,
                 counts, s, cm);
   if (A > 0 && !best && !multi)  // else the keys came from the Detect cls epilogue (fce_nms_best)

@@ -119,6 +119,24 @@ class _Stage:
             self.dev = torch.empty(cap, dtype=torch.uint8, device=device)
 
 
+def default_lanes(model) -> int:
+    """Batches in flight for a model: 5 on the n / s scales, 3 on m / l / x (see Predictor)."""
+    scale = (getattr(model, "yaml", None) or {}).get("scale") or "n"
+    return 5 if scale in ("n", "s") else 3
+
+
+def _host_image(im) -> np.ndarray:
+    """A decoded image as a C-contiguous host array: numpy arrays and CPU tensors are accepted; a tensor on a
+    device is refused (this path packs host images into pinned staging; device-resident images go through
+    `Letterbox` + `Engine` + `NMS` directly)."""
+    if isinstance(im, torch.Tensor):
+        if im.device.type != "cpu":
+            raise TypeError(f"Predictor: images must be host arrays (numpy or CPU tensors), got a {im.device} tensor; "
+                            "for device-resident images use predict.Letterbox + Engine + NMS")
+        im = im.numpy()
+    return np.ascontiguousarray(im)
+
+
 class Predictor:
     """predict(images) -> per image (k, 6) [x1, y1, x2, y2, conf, cls] in source pixels (+ anchor indices).
 
@@ -138,15 +156,19 @@ class Predictor:
     collected when the lane is reused are kept on the host.  A call with fewer images than `batch` repeats the
     last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
 
-    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300, lanes: int = 5,
-                 graph: bool = True, workers: int | None = None, copy_stream: bool = True):
-        """`lanes`: batches on the device at once (5: measured best for 32 x 480x640 images, scripts/predict_diag.py).
+    def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300,
+                 lanes: int | None = None, graph: bool = True, workers: int | None = None, copy_stream: bool = True):
+        """`lanes`: batches on the device at once; default by scale (`default_lanes`): 5 on the n / s scales
+        (measured best for 32 x 480x640 images, scripts/predict_diag.py), 3 on m / l, where every lane's
+        activation arena is large and more than three arenas overflow the MALL (bench.default_lanes).
         `workers`: host threads packing images into pinned memory (default min(8, cpus / 2); 4-8 reach ~31 GB/s
         on the MI355X box).  `copy_stream` (default): every H2D copy on one dedicated stream, lanes wait on it
         (18.9k against 15.9k images/s with the copy on the lane's own stream, scripts/predict_diag.py)."""
         import os
         from concurrent.futures import ThreadPoolExecutor
 
+        if lanes is None:
+            lanes = default_lanes(model)
         self.engine = Engine(model, batch, imgsz, device, graph=graph)
         self.device = self.engine.device
         self.batch = batch
@@ -175,7 +197,7 @@ class Predictor:
         Returns the record _issue consumes; the packing runs while the caller does other work."""
         if not 0 < len(images) <= self.batch:
             raise ValueError(f"Predictor: 1..{self.batch} images per call")
-        imgs = [np.ascontiguousarray(im) for im in images]
+        imgs = [_host_image(im) for im in images]
         for im in imgs:
             if im.dtype != np.uint8 or im.ndim != 3 or im.shape[2] != 3:
                 raise ValueError("Predictor: images must be uint8 (h, w, 3) BGR arrays")
@@ -277,7 +299,8 @@ class Predictor:
         return res
 
     def result(self, ticket: int, return_idxs: bool = False):
-        """Per image (k, 6) host tensors of a submitted batch (+ kept anchor indices)."""
+        """Per image (k, 6) HOST tensors of a submitted batch (+ kept anchor indices): the packed detections come
+        back in one D2H copy per batch; `.to(device)` them if the caller's next step is on the GPU."""
         if ticket in self._ready:
             d, k = self._ready.pop(ticket)
         else:

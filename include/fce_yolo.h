@@ -101,6 +101,12 @@ int fce_conv_variants(const fce_conv_desc* d, int in_w, int* codes, int cap);
 /* fce_conv2d with an explicit variant code from fce_conv_variants (-1 = heuristic). */
 int fce_conv2d_variant(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
                        const fce_tensor* residual, const fce_tensor* y, int variant, void* stream);
+/* fce_conv2d_variant of a plain 1x1 conv whose epilogue also stores output channels [dup_lo, dup_lo + dup->c)
+ * into the dense view dup (the C2f / C3k2 cv1 duplicate store of fce_net_add_conv_dup; dup_lo, dup->c % 8 == 0):
+ * every variant's store path writes the same fp16 values to both. */
+int fce_conv2d_variant_dup(const fce_conv_desc* d, const fce_tensor* x, const void* w_packed, const float* bias,
+                           const fce_tensor* residual, const fce_tensor* y, int variant, const fce_tensor* dup,
+                           int dup_lo, void* stream);
 
 /* Detect tail fused into the last 1x1 conv of a branch (head.py:149-167): part 0 = box branch
  * (4*reg_max logits -> DFL expectation -> xywh * stride into pred rows 0..3), part 1 = cls branch

@@ -224,11 +224,16 @@ def test_full_size_op_parity(key, full_fx, device):
     assert err <= OP_TOL and e_slice <= OP_TOL and e_sum <= OP_TOL, (err, e_slice, e_sum)
 
 
-@pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11s-bifpn.yaml", 2, 256),
-                                             ("yolo11n-fce.yaml", 1, 224)])
-def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, device, monkeypatch):
-    """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give
-    (partial edge tiles at 224: 56 = 3.5 x 16), whole-graph and per-module."""
+@pytest.mark.parametrize("cfg,batch,imgsz,tile", [
+    ("yolo11n-fce.yaml", 2, 320, None), ("yolo11s-bifpn.yaml", 2, 256, None), ("yolo11n-fce.yaml", 1, 640, None),
+    ("yolo11n-fce.yaml", 1, 224, None), ("yolo11n-fce.yaml", 1, 224, "8,16,4"), ("yolo11n-fce.yaml", 1, 224, "4,40,8"),
+    ("yolo11n-fce.yaml", 1, 224, "2,16,8"), ("yolo11n-fce.yaml", 2, 160, "8,32,4")])
+def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device, monkeypatch):
+    """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give, whole-graph
+    and per-module; every tile shape the planner picks (8 x 16 on 160^2 maps, 4 x 40 below), forced shapes
+    (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40)."""
+    if tile:
+        monkeypatch.setenv("FCE_C3K2_TILE", tile)
     model = cases.seeded_model(cfg, 0).to(device)
     x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(9)).half().to(device)
     monkeypatch.setenv("FCE_FUSE_C3K2", "1")
@@ -649,6 +654,21 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
     for code, y in outs.items():
         assert torch.equal(y, base), (hex(code), (y.float() - base.float()).abs().max().item())
     assert _rel(base, ref) <= 4e-3
+    if epi != N.EPI_STORE:
+        return
+    # the duplicate store (C2f / C3k2 cv1, fce_net_add_conv_dup) through every variant's store path: the dense
+    # copy equals the output's channels [lo, lo + dc) and the output itself is unchanged
+    lo, dc = 8, min(16, cout - 8)
+    for code in [-1] + list(codes[:nv]):
+        y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
+        dup = torch.full((2, Ho, Wo, dc), float("nan"), dtype=torch.float16, device=device)
+        yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout + ypad, ypad)
+        dt = N.Tensor(dup.data_ptr(), N.F16, N.NHWC, 2, dc, Ho, Wo, dc, 0)
+        N.call("fce_conv2d_variant_dup", C.byref(desc), C.byref(xt), wp.data_ptr(), bd.data_ptr(), None, C.byref(yt),
+               code, C.byref(dt), lo, None)
+        yc = y.cpu()
+        assert torch.equal(yc[..., ypad:].permute(0, 3, 1, 2), base), hex(code)
+        assert torch.equal(dup.cpu(), yc[..., ypad + lo:ypad + lo + dc]), hex(code)
 
 
 @pytest.mark.parametrize("case", CONV_VARIANT_CASES)
