@@ -157,14 +157,23 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--profile-json", default=None, help="write the per-op profile here")
     ap.add_argument("--profile-passes", type=int, default=10, help="per-op HIP-event passes averaged")
-    ap.add_argument("--predict-lanes", type=int, default=5, help="batches in flight in the host-image predict leg")
+    ap.add_argument("--predict-lanes", type=int, default=None,
+                    help="batches in flight in the host-image legs (default predict.default_lanes: 5 on n / s, 3 on m / l)")
     ap.add_argument("--predict-steps", type=int, default=30,
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
+    ap.add_argument("--source", choices=("device", "host"), default="device",
+                    help="device (default, the contract line): resident fp16 inputs; host: every rank predicts its "
+                         "contiguous shard of decoded uint8 host images (dist.ShardedHostPredictor: H2D, letterbox, "
+                         "forward, NMS, scale_boxes, per-batch gather of the detections) -- PCIe inclusive, not `value` "
+                         "of the contract line")
     a = ap.parse_args()
     if a.lanes is None:
         a.lanes = default_lanes(a.model, os.environ, a.gpus)
     if a.graph < 0:
         a.graph = 1 if a.lanes > 1 else 0
+    if a.predict_lanes is None:
+        stem = Path(a.model).stem
+        a.predict_lanes = 5 if (stem[6:7] if stem.startswith("yolo11") else "n") in ("n", "s") else 3
     return a
 
 
@@ -251,6 +260,59 @@ def cpu_baseline(model_name: str, imgsz: int, seconds: float, batch: int = 32):
     }
 
 
+def host_source_line(a, model, rank, world, use_dist, dev):
+    """--source host: the sharded host-image path, one JSON line (PCIe inclusive)."""
+    import numpy as np
+
+    from fce_yolo_amd.dist import ShardedHostPredictor
+
+    B, S = a.batch, a.imgsz
+    sp = ShardedHostPredictor(model, B * world, S, dev, batch_size=B, lanes=a.predict_lanes, workers=4)
+    # each rank decodes (synthesises) only its own shard: image i of a global batch is seeded by i
+    shard = [np.random.default_rng(i).integers(0, 256, (480, 640, 3), dtype=np.uint8) for i in range(sp.start, sp.end)]
+
+    def run(n):
+        k = 0
+        for dets, _ in sp.stream(shard for _ in range(n)):
+            k += len(dets)
+        return k
+
+    run(max(2, a.warmup))
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = run(a.steps)
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if use_dist and dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elif use_dist:
+        t = t.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    assert n == B * world * a.steps
+    sp.close()
+    stem = Path(a.model).stem
+    return {
+        "metric": "images/sec/GPU @ 640x640 bs=32, yolo11n-fce; fraction of fp16 MFMA roofline",
+        "value": round(B * world * a.steps / el, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp16",
+        "data": "synthetic decoded 480x640 uint8 BGR host images, each rank generating only its own shard",
+        "config": {"workload": f"{stem} detection predict from host images (H2D + letterbox + forward + NMS + "
+                               f"scale_boxes + gather) @ {S}x{S}, {B} images/GPU", "model": stem,
+                   "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}", "source": "host",
+                   "batches_in_flight": a.predict_lanes},
+        "note": "PCIe-inclusive host-image path (--source host), not the resident-input contract line",
+        "process_group": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()} if use_dist
+                          else None),
+    }
+
+
 def main():
     a = parse_args()
     rank = int(os.environ.get("RANK", 0))
@@ -284,6 +346,14 @@ def main():
         broadcast_module(model, src=0)
 
     B, S = a.batch, a.imgsz
+    if a.source == "host":
+        out = host_source_line(a, model, rank, world, use_dist, dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if use_dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     # this rank's contiguous shard of a global batch of B * world images (dist.ShardedPredictor)
     sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")),
                           lanes=a.lanes, gather=use_dist)

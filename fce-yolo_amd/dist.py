@@ -188,3 +188,90 @@ class ShardedPredictor:
         torch.cuda.synchronize(self.engine.device)
         for e in self.pipe.engs:
             e.close()
+
+
+def pack_detections(dets, keep, bmax: int, max_det: int):
+    """Per-image (k, 6) detections + kept anchor indices -> (counts (bmax,), dets (bmax, max_det, 6) f32,
+    keep (bmax, max_det) int64), zero padded: the fixed-size form every rank sends in a gather."""
+    counts = torch.zeros(bmax, dtype=torch.int64)
+    d = torch.zeros((bmax, max_det, 6), dtype=torch.float32)
+    k = torch.zeros((bmax, max_det), dtype=torch.int64)
+    for i, (di, ki) in enumerate(zip(dets, keep)):
+        n = int(di.shape[0])
+        counts[i] = n
+        d[i, :n] = di.to("cpu", torch.float32)
+        k[i, :n] = ki.to("cpu", torch.int64)
+    return counts, d, k
+
+
+class ShardedHostPredictor:
+    """The host-image predict path sharded over ranks ("each rank loads its own shard").
+
+    Rank r takes its contiguous shard (`shard_range`, the reference's ContiguousDistributedSampler rule,
+    data/build.py:115-215) of every global batch of decoded uint8 HWC BGR images and runs it through
+    `predict.Predictor` (pinned staging -> one H2D -> device letterbox -> forward -> NMS -> scale_boxes, several
+    batches in flight; the reference's predictor.py:151-182 preprocess + inference + postprocess).  The per-image
+    detections of every rank are all-gathered once per batch (fixed-size packed tensors: RCCL over xGMI on the
+    device for the nccl backend, host tensors for gloo), so `stream` yields each global batch's results in the
+    unsharded image order on every rank -- what one Predictor over the whole batch returns.  Images never cross
+    GPUs; only ~7 KB of detections per image do."""
+
+    def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, lanes: int | None = None,
+                 gather: bool | None = None, predictor=None, max_det: int = 300, **kw):
+        """`predictor(batch)` builds the per-rank predictor (default: predict.Predictor(model, batch, imgsz,
+        device, lanes=lanes, max_det=max_det, **kw)); anything with `stream(batches, return_idxs=True)` and
+        `close()` fits (tests use a host stub)."""
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.do_gather = self.world > 1 if gather is None else bool(gather) and dist.is_initialized()
+        bs = batch_size or -(-total // self.world)
+        self.total = total
+        self.sizes = shard_sizes(total, self.world, bs)
+        self.start, self.end = shard_range(total, self.world, self.rank, bs)
+        self.batch = self.end - self.start
+        if min(self.sizes) <= 0:  # decided from sizes every rank computes alike: all ranks raise, none hangs
+            raise ValueError(f"empty shard(s) {self.sizes} of a {total}-image batch over {self.world} ranks")
+        self.bmax = max(self.sizes)
+        self.max_det = max_det
+        if predictor is None:
+            from .predict import Predictor
+
+            self.pred = Predictor(model, self.batch, imgsz, device, lanes=lanes, max_det=max_det, **kw)
+        else:
+            self.pred = predictor(self.batch)
+        backend = dist.get_backend() if dist.is_initialized() else "gloo"
+        self.comm_device = torch.device(device) if backend == "nccl" else torch.device("cpu")
+
+    def shard(self, images):
+        """This rank's images of a global batch (a full batch of `total` images, or already just the shard)."""
+        if len(images) == self.batch and self.total != self.batch:
+            return list(images)
+        if len(images) != self.total:
+            raise ValueError(f"rank {self.rank}: a global batch of {self.total} images (or its {self.batch}-image "
+                             f"shard) expected, got {len(images)}")
+        return list(images[self.start:self.end])
+
+    def _gather(self, dets, keep):
+        if not self.do_gather:
+            return dets, keep
+        packed = [t.to(self.comm_device) for t in pack_detections(dets, keep, self.bmax, self.max_det)]
+        outs = []
+        for t in packed:
+            bufs = [torch.empty_like(t) for _ in range(self.world)]
+            dist.all_gather(bufs, t)
+            outs.append([b.cpu() for b in bufs])
+        res_d, res_k = [], []
+        for r, n in enumerate(self.sizes):
+            cnt = outs[0][r][:n].tolist()
+            res_d += [outs[1][r][i, :cnt[i]] for i in range(n)]
+            res_k += [outs[2][r][i, :cnt[i]] for i in range(n)]
+        return res_d, res_k
+
+    def stream(self, batches):
+        """Per global batch, (dets, keep) per image of the whole batch in the unsharded order.  Every rank must
+        be given the same number of batches (the gather is collective)."""
+        for dets, keep in self.pred.stream((self.shard(b) for b in batches), return_idxs=True):
+            yield self._gather(dets, keep)
+
+    def close(self):
+        self.pred.close()

@@ -201,6 +201,38 @@ E2E_NMS = {
 }
 
 
+E2E_NMS640 = {
+    # fixture key: (cfg, batch, imgsz) -- make_golden_e2e_nms640.CASES (per-image input seeds)
+    "yolo11n-fce_640_b32": ("yolo11n-fce.yaml", 32, 640),
+    "yolo11s-bifpn_640_b4": ("yolo11s-bifpn.yaml", 4, 640),
+}
+
+
+def designed_model640(key, fx):
+    """(model, input) of a headline-size margin-designed case (make_golden_e2e_nms640.py): the designed Detect cls
+    convs on seeded_state_dict(keys, 0, gain), and the batch of per-image seeded inputs."""
+    import re
+
+    from fce_yolo_amd.parser import DetectionModel, load_cfg
+
+    cfg, b, s = E2E_NMS640[key]
+    model = DetectionModel(load_cfg(cfg))
+    sd = seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0, gain=float(fx["gain"]))
+    det = len(model.model) - 1
+    n = 0
+    for k in sd:
+        m = re.match(rf"^model\.{det}\.cv3\.(\d+)\.2\.(weight|bias)$", k)
+        if m:
+            sd[k] = torch.from_numpy(fx[f"cls_{m.group(2)[0]}{m.group(1)}"].copy())
+            n += 1
+    assert n == 6, n
+    model.load_state_dict(sd)
+    seeds = [int(v) for v in fx["seeds"]]
+    assert len(seeds) == b
+    x = torch.cat([torch.rand(1, 3, s, s, generator=torch.Generator().manual_seed(v)) for v in seeds])
+    return model.eval(), x
+
+
 def designed_model(key, fx):
     """(model, input) of a margin-designed end-to-end NMS case: seeded_state_dict(keys, 0, gain) with the
     Detect cls head's last 1x1 convs replaced by the fixture's designed weights (make_golden_e2e_nms.py)."""

@@ -58,6 +58,11 @@ def e2e_nms_fx():
 
 
 @pytest.fixture(scope="session")
+def e2e_nms640_fx():
+    return _Npz(GOLDEN / "e2e_nms640.npz")
+
+
+@pytest.fixture(scope="session")
 def nms_fx():
     return _Npz(GOLDEN / "nms.npz")
 

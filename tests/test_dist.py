@@ -158,3 +158,76 @@ def test_sharded_predictor_empty_shard_raises_on_every_rank_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == [(0, "ValueError"), (1, "ValueError")]
+
+
+class _StubPredictor:
+    """Host stand-in for predict.Predictor (no GPU here): per image a deterministic function of the image's pixels
+    -> (k, 6) rows and k anchor indices, k = 1 + (first pixel % 4); `stream` keeps Predictor's contract (one
+    (dets, keep) pair of per-image lists per batch, in order)."""
+
+    def __init__(self, batch):
+        self.batch = batch
+
+    @staticmethod
+    def one(im):
+        t = torch.from_numpy(im.astype("float32"))
+        k = 1 + int(im.flat[0]) % 4
+        d = torch.stack([t.mean() + j + torch.arange(6, dtype=torch.float32) for j in range(k)])
+        return d, torch.arange(k, dtype=torch.int64) * 7 + int(im.flat[1])
+
+    def stream(self, batches, return_idxs=True):
+        for b in batches:
+            assert 0 < len(b) <= self.batch
+            r = [self.one(im) for im in b]
+            yield [x[0] for x in r], [x[1] for x in r]
+
+    def close(self):
+        pass
+
+
+def _host_batches(total, nb):
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    return [[rng.integers(0, 256, (6 + i % 3, 5 + i % 2, 3), dtype=np.uint8) for i in range(total)] for _ in range(nb)]
+
+
+def _host_worker(rank, world, port, q, total, bs):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fce_yolo_amd.dist import ShardedHostPredictor
+
+        sp = ShardedHostPredictor(None, total, 640, "cpu", batch_size=bs, predictor=_StubPredictor)
+        batches = _host_batches(total, 3)
+        # rank 0 is handed whole global batches, rank 1 only its own shards ("each rank loads its own shard")
+        feed = batches if rank == 0 else [b[sp.start:sp.end] for b in batches]
+        out = [([d.tolist() for d in ds], [k.tolist() for k in ks]) for ds, ks in sp.stream(feed)]
+        q.put((rank, (sp.start, sp.end), out))
+        sp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,bs", [(7, 4), (6, 32)])
+def test_sharded_host_predictor_matches_one_rank_gloo_world2(total, bs):
+    """dist.ShardedHostPredictor over two gloo ranks: each rank predicts only its contiguous shard (uneven at 7
+    images), and the all-gathered per-image results equal one predictor over every whole batch, in order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, 2, port, q, total, bs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    one = _StubPredictor(total)
+    want = []
+    for b in _host_batches(total, 3):
+        ds, ks = next(one.stream([b]))
+        want.append(([d.tolist() for d in ds], [k.tolist() for k in ks]))
+    (r0, rng0, out0), (r1, rng1, out1) = res
+    assert rng0 == shard_range(total, 2, 0, bs) and rng1 == shard_range(total, 2, 1, bs)
+    assert out0 == want and out1 == want

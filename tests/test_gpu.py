@@ -582,6 +582,60 @@ def test_end_to_end_nms_indices_bit_exact_vs_reference(key, e2e_nms_fx, device):
                 assert np.abs(d[:, 4] - r[:, 4]).max() <= float(fx["score_margin"])
 
 
+@pytest.mark.parametrize("key", list(cases.E2E_NMS640))
+def test_end_to_end_nms_indices_640_in_the_shipped_modes(key, e2e_nms640_fx, device):
+    """Kept anchor indices bit-equal to the reference's at the HEADLINE size (make_golden_e2e_nms640.py: yolo11n-fce
+    640 x 640 with the bench's batch of 32, yolo11s-bifpn 640 batch 4; the 20 x 20 level's 8 designed classes, per
+    image margins), through every way the bench and the multi-GPU path run the forward: one executor (graph replay
+    and direct launches, NMS with and without the epilogue's best-class keys), engine.Pipeline with four lanes each
+    replaying its own captured hipGraph (bench.py's default on one GPU) with fresh inputs dropped after submit, and
+    dist.ShardedPredictor on one rank (the bench's step object)."""
+    from fce_yolo_amd.dist import ShardedPredictor
+
+    fx = e2e_nms640_fx.group(key)
+    model, x = cases.designed_model640(key, fx)
+    _, B, S = cases.E2E_NMS640[key]
+    a0, ref_y = int(fx["anchor0"]), fx["y_level"]
+    model = model.to(device)
+    xd = x.half().to(device)
+
+    def check(tag, dets, keep):
+        for b in range(B):
+            k, d, r = keep[b].cpu().numpy(), dets[b].cpu().numpy(), fx[f"det{b}"]
+            assert np.array_equal(k, fx[f"keep{b}"]), (tag, b, k, fx[f"keep{b}"])
+            assert np.array_equal(d[:, 5], r[:, 5]), (tag, b)
+            assert np.abs(d[:, :4] - r[:, :4]).max() <= BOX_TOL * np.abs(r[:, :4]).max(), (tag, b)
+            assert np.abs(d[:, 4] - r[:, 4]).max() <= float(fx["score_margin"]), (tag, b)
+
+    eng = Engine(model, B, S, device)
+    for graph in (True, False):
+        best = eng.new_best()
+        pred = eng(xd, out=torch.empty_like(eng.pred), best=best, graph=graph)
+        torch.cuda.synchronize()
+        yl = pred[:, :ref_y.shape[1], a0:a0 + ref_y.shape[2]].cpu().numpy()
+        print(f"{key} graph={graph}: score err {np.abs(yl[:, 4:] - ref_y[:, 4:]).max():.2e}, box rel "
+              f"{np.abs(yl[:, :4] - ref_y[:, :4]).max() / np.abs(ref_y[:, :4]).max():.2e}, kept "
+              f"{[len(fx[f'keep{b}']) for b in range(B)]}")
+        for use_best in (False, True):
+            nms = NMS(B, eng.anchors, eng.nc, device)
+            nms(pred, best if use_best else None)
+            check(f"engine graph={graph} best={use_best}", *nms.results())
+    pipe = Pipeline(eng, depth=4, lanes=4)
+    for e in pipe.engs:
+        e.graph = True
+    slots = [pipe.submit(x.half().to(device)) for _ in range(6)]  # fresh inputs, dropped right after submit
+    for i in range(len(slots) - pipe.depth, len(slots)):
+        check(f"pipeline slot {i}", *pipe.results(slots[i]))
+    eng.close()
+    sp = ShardedPredictor(model, B, S, device, lanes=4)
+    for e in sp.pipe.engs:
+        e.graph = True
+    slots = [sp.submit(xd) for _ in range(5)]
+    for i in range(len(slots) - sp.pipe.depth, len(slots)):
+        check(f"sharded slot {i}", *sp.results(slots[i]))
+    sp.close()
+
+
 CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (8, 8, 3, 1, 37, 45, True), (16, 32, 3, 2, 40, 50, False), (8, 16, 3, 1, 33, 20, False),
     (48, 64, 3, 1, 21, 35, False), (24, 40, 3, 2, 19, 31, False), (64, 64, 3, 1, 40, 40, True),

@@ -1,0 +1,84 @@
+"""GPU, two processes: the sharded host-image predict path (dist.ShardedHostPredictor) with the real
+predict.Predictor on each rank, both ranks on cuda:0 over gloo (the one-GPU box rehearsal of the multi-GPU path;
+RCCL replaces gloo on an 8-GPU node), against one Predictor over the whole batches."""
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import fce_pkg  # noqa: E402  (spawned workers import this module fresh)
+
+fce_pkg.load()
+
+pytestmark = pytest.mark.gpu
+TOTAL, BS, S = 7, 4, 256
+
+
+def _model():
+    from fce_yolo_amd.parser import DetectionModel
+    from fce_yolo_amd.weights import seeded_state_dict
+
+    m = DetectionModel("yolo11n-fce.yaml")
+    m.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in m.state_dict().items()], 0, gain=1.45))
+    return m.eval().to("cuda:0")
+
+
+def _batches(nb=3):
+    rng = np.random.default_rng(11)
+    return [[rng.integers(0, 256, (200 + 17 * i, 300 - 9 * i, 3), dtype=np.uint8) for i in range(TOTAL)]
+            for _ in range(nb)]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fce_yolo_amd.dist import ShardedHostPredictor
+
+        torch.cuda.set_device(0)
+        sp = ShardedHostPredictor(_model(), TOTAL, S, "cuda:0", batch_size=BS, lanes=2, conf=0.05)
+        out = [([d.numpy() for d in ds], [k.numpy() for k in ks]) for ds, ks in sp.stream(_batches())]
+        q.put((rank, out))
+        sp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_host_predictor_two_ranks_match_one_predictor():
+    from fce_yolo_amd.predict import Predictor
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    pred = Predictor(_model(), TOTAL, S, "cuda:0", lanes=2, conf=0.05)
+    want = list(pred.stream(_batches(), return_idxs=True))
+    pred.close()
+    assert sum(len(d) for ds, _ in want for d in ds) > 0  # the seeded head keeps some boxes
+    for rank, out in res:
+        assert len(out) == len(want)
+        for (ds, ks), (wd, wk) in zip(out, want):
+            assert len(ds) == TOTAL
+            for d, k, d1, k1 in zip(ds, ks, wd, wk):
+                assert np.array_equal(k, k1.numpy()), rank
+                assert np.array_equal(d, d1.numpy()), rank

@@ -107,6 +107,22 @@ def test_oracle_designed_end_to_end_nms_matches_reference(key, e2e_nms_fx):
         assert np.abs(dets[b] - fx[f"det{b}"]).max() <= 1e-4 * max(1.0, np.abs(fx[f"det{b}"]).max()), b
 
 
+@pytest.mark.parametrize("key", list(cases.E2E_NMS640))
+def test_oracle_designed_end_to_end_nms_640_matches_reference(key, e2e_nms640_fx):
+    """Headline-size margin-designed case (make_golden_e2e_nms640.py: n-fce 640 batch 32, s-bifpn 640 batch 4):
+    the oracle's fp32 forward + oracle NMS keep exactly the reference's anchors, rows to 1e-4."""
+    fx = e2e_nms640_fx.group(key)
+    model, x = cases.designed_model640(key, fx)
+    y = cases.oracle_model(model, x, torch.float32).numpy()
+    a0, ref = int(fx["anchor0"]), fx["y_level"]
+    yl = y[:, :ref.shape[1], a0:a0 + ref.shape[2]]
+    assert np.abs(yl - ref).max() <= 1e-4 * np.abs(ref).max()
+    dets, keeps = nms_oracle.non_max_suppression(y)
+    for b in range(x.shape[0]):
+        assert np.array_equal(keeps[b], fx[f"keep{b}"]), b
+        assert np.abs(dets[b] - fx[f"det{b}"]).max() <= 1e-4 * max(1.0, np.abs(fx[f"det{b}"]).max()), b
+
+
 def _cfg(name):
     """The built-in graph data of the product package (restated from the reference YAMLs)."""
     from fce_yolo_amd.parser import load_cfg
