@@ -134,6 +134,10 @@ _SIGS = {
     "fce_c3k2_supported": (_I, [_PC3]),
     "fce_c3k2": (_I, [_PC3, _PT, _PT, _P]),
     "fce_net_add_c3k2": (_I, [_P, _PC3, _I, _I, _I, _I]),
+    "fce_net_add_c3k2_alt": (_I, [_P, _PC3, _I, _I, _I, _I, _I, _I]),
+    "fce_net_c3k2_form": (_I, [_P, _I]),
+    "fce_net_set_c3k2_form": (_I, [_P, _I, _I]),
+    "fce_net_op_skipped": (_I, [_P, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

@@ -277,6 +277,14 @@ class NetBackend:
     def c3k2(self, desc: N.C3k2Desc, x: View, y: View):
         N.call("fce_net_add_c3k2", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff)
 
+    def num_ops(self) -> int:
+        return N.lib().fce_net_num_ops(self.net)
+
+    def c3k2_alt(self, desc: N.C3k2Desc, x: View, y: View, first_op: int, nops: int):
+        """The fused C3k2 as the alternative of ops [first_op, first_op + nops) (its four convs): the plan-time
+        autotune keeps the faster form (fce_net_add_c3k2_alt)."""
+        N.call("fce_net_add_c3k2_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
+
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         assert qkv.coff == 0 and qkv.c == qkv.cstride
         N.call("fce_net_add_psa_attention", self.net, qkv.buf, heads, kd, hd, pe_w, pe_b, y.buf, y.coff)

@@ -238,6 +238,10 @@ struct OpDesc {
   fce_c3k2_desc c3k2{};              // OP_C3K2
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
   int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
+  // alternative forms: an OP_C3K2 added by fce_net_add_c3k2_alt computes the same output as ops [alt_first,
+  // alt_first + alt_n) (its four convs); exactly one form runs, the other's ops are skipped (plan-time choice)
+  int alt_first = -1, alt_n = 0;
+  bool skip = false;
 };
 
 }  // namespace
@@ -349,7 +353,7 @@ int op_input_view(const fce_net* net, const OpDesc& op, const fce_tensor& input,
   return FCE_OK;
 }
 
-int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred, hipStream_t s) {
+int run_op_impl(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred, hipStream_t s) {
   fce_tensor x;
   op_input_view(net, op, input, &x);
   switch (op.kind) {
@@ -409,6 +413,11 @@ int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred,
   return fail(FCE_ERR_INVALID, "unknown op");
 }
 
+// an op of the inactive form of an alternative launches nothing
+int run_op(fce_net* net, const OpDesc& op, const fce_tensor& input, float* pred, hipStream_t s) {
+  return op.skip ? FCE_OK : run_op_impl(net, op, input, pred, s);
+}
+
 int run_all(fce_net* net, const fce_tensor& input, float* pred, hipStream_t s, bool fork = false) {
   for (size_t i = 0; i < net->ops.size(); ++i) {
     int st = run_op(net, net->ops[i], input, pred, s);
@@ -430,6 +439,7 @@ static constexpr int kBufPred = -2, kBufWs = -3, kBufBest = -4;
 
 static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access>& a) {
   a.clear();
+  if (op.skip) return;
   switch (op.kind) {
     case OP_CONV:
       if (op.in >= 0) a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
@@ -535,6 +545,13 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
   auto hw = [&](int id) { return double(net->H >> net->bufs[id].shift) * double(net->W >> net->bufs[id].shift); };
   *bytes = 0;
   *flops = 0;
+  if (op.skip) {  // the inactive form of an alternative: its name, no work
+    double b, f;
+    OpDesc live = op;
+    live.skip = false;
+    op_cost(net, live, name, &b, &f);
+    return;
+  }
   switch (op.kind) {
     case OP_CONV: {
       const fce_conv_desc& d = op.conv;
@@ -605,6 +622,13 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       break;
     }
   }
+}
+
+// the active form of an alternative: the fused op, or the convs it replaces
+void set_c3k2_form(fce_net* net, OpDesc& op, bool fused) {
+  if (op.skip != !fused) net->drop_graph();  // captured forwards hold the other form's launches
+  op.skip = !fused;
+  for (int j = op.alt_first; j < op.alt_first + op.alt_n; ++j) net->ops[j].skip = fused;
 }
 
 }  // namespace
@@ -773,6 +797,38 @@ int fce_net_add_psa_attention(fce_net* net, int qkv, int heads, int kd, int hd, 
   return FCE_OK;
 }
 
+int fce_net_add_c3k2_alt(fce_net* net, const fce_c3k2_desc* d, int in, int in_coff, int out, int out_coff,
+                         int first_op, int nops) {
+  FCE_CHECK(net && nops >= 1 && first_op >= 0 && first_op + nops == int(net->ops.size()),
+            "fce_net_add_c3k2_alt: the alternative must be the last ops added");
+  for (int j = first_op; j < first_op + nops; ++j)
+    FCE_CHECK(net->ops[j].kind == OP_CONV && !net->ops[j].skip && net->ops[j].alt_first < 0,
+              "fce_net_add_c3k2_alt: the alternative must be plain conv ops");
+  const int st = fce_net_add_c3k2(net, d, in, in_coff, out, out_coff);
+  if (st) return st;
+  OpDesc& op = net->ops.back();
+  op.alt_first = first_op;
+  op.alt_n = nops;
+  set_c3k2_form(net, op, true);  // fused until the plan-time autotune says otherwise
+  return FCE_OK;
+}
+
+int fce_net_c3k2_form(const fce_net* net, int i) {
+  if (!net || i < 0 || i >= int(net->ops.size())) return -1;
+  const OpDesc& op = net->ops[i];
+  return op.kind == OP_C3K2 && op.alt_first >= 0 ? (op.skip ? 0 : 1) : -1;
+}
+
+int fce_net_set_c3k2_form(fce_net* net, int i, int fused) {
+  FCE_CHECK(fce_net_c3k2_form(net, i) >= 0, "fce_net_set_c3k2_form: not a fused C3k2 op with an alternative");
+  set_c3k2_form(net, net->ops[i], fused != 0);
+  return FCE_OK;
+}
+
+int fce_net_op_skipped(const fce_net* net, int i) {
+  return net && i >= 0 && i < int(net->ops.size()) && net->ops[i].skip ? 1 : 0;
+}
+
 int fce_net_add_c3k2(fce_net* net, const fce_c3k2_desc* d, int in, int in_coff, int out, int out_coff) {
   FCE_CHECK(net && d && valid_buf(net, in, false) && valid_buf(net, out, false), "fce_net_add_c3k2: bad argument");
   FCE_CHECK(c3k2_fused_ok(*d), "fce_net_add_c3k2: unsupported channel configuration");
@@ -868,13 +924,13 @@ static int autotune(fce_net* net) {
     int best = -1;
     for (int i = 0; i < nc_ && st == FCE_OK; ++i) {
       op.tile = cand[i];
-      for (int r = 0; r < 2 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
+      for (int r = 0; r < 2 && st == FCE_OK; ++r) st = run_op_impl(net, op, none, pred, ts);
       if (st) break;
       // best of two 3-launch windows: one window alone let clock / co-tenant noise flip close picks
       float ms = 1e30f;
       for (int t = 0; t < 2 && st == FCE_OK; ++t) {
         (void)hipEventRecord(e0, ts);
-        for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_op(net, op, none, pred, ts);
+        for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_op_impl(net, op, none, pred, ts);
         (void)hipEventRecord(e1, ts);
         if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
         float w = 0.f;
@@ -889,6 +945,37 @@ static int autotune(fce_net* net) {
     }
     op.tile = best;
     if (st) break;
+  }
+  // alternative forms (fused C3k2 against its four tuned convs): time both on the planned shapes, keep the faster
+  // (FCE_FUSE_C3K2=1 keeps the fused form without timing).  Logged as codes 0xF01 (fused) / 0xF00 (the convs).
+  const char* fe = getenv("FCE_FUSE_C3K2");
+  const bool force_fused = fe && strcmp(fe, "1") == 0;
+  for (size_t i = 0; i < net->ops.size() && st == FCE_OK && !force_fused; ++i) {
+    OpDesc& op = net->ops[i];
+    if (op.kind != OP_C3K2 || op.alt_first < 0) continue;
+    float t[2] = {1e30f, 1e30f};  // [convs, fused]
+    for (int form = 0; form < 2 && st == FCE_OK; ++form) {
+      auto run_form = [&]() {
+        if (form == 1) return run_op_impl(net, op, none, pred, ts);
+        for (int j = op.alt_first; j < op.alt_first + op.alt_n; ++j) {
+          const int r = run_op_impl(net, net->ops[j], none, pred, ts);
+          if (r) return r;
+        }
+        return FCE_OK;
+      };
+      for (int r = 0; r < 2 && st == FCE_OK; ++r) st = run_form();
+      for (int w = 0; w < 2 && st == FCE_OK; ++w) {
+        (void)hipEventRecord(e0, ts);
+        for (int r = 0; r < 3 && st == FCE_OK; ++r) st = run_form();
+        (void)hipEventRecord(e1, ts);
+        if (hipEventSynchronize(e1) != hipSuccess) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune sync failed");
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        t[form] = std::min(t[form], ms / 3.f);
+      }
+      if (st == FCE_OK) net->tune_log.push_back({int(i), 0xF00 | form, t[form]});
+    }
+    if (st == FCE_OK) set_c3k2_form(net, op, t[1] <= t[0]);
   }
   if (hipStreamSynchronize(ts) != hipSuccess && st == FCE_OK) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune failed");
   cleanup();

@@ -93,7 +93,21 @@ class Engine:
         for i in range(self.num_ops()):
             if self.variants(i):
                 e.set_variant(i, self.variant(i))
+            f = self.c3k2_form(i)
+            if f >= 0:
+                e.set_c3k2_form(i, bool(f))
         return e
+
+    def c3k2_form(self, i: int) -> int:
+        """1: op i (a fused C3k2 with its four convs as the alternative) runs fused; 0: the convs run; -1: other op."""
+        return N.lib().fce_net_c3k2_form(self.be.net, i)
+
+    def set_c3k2_form(self, i: int, fused: bool) -> None:
+        N.call("fce_net_set_c3k2_form", self.be.net, i, int(bool(fused)))
+
+    def skipped(self, i: int) -> bool:
+        """Op i belongs to the inactive form of an alternative (launches nothing)."""
+        return bool(N.lib().fce_net_op_skipped(self.be.net, i))
 
     def profile(self, x: torch.Tensor, launches: bool = False):
         """Eager run, every kernel timed by its own dispatch-attached event pair:

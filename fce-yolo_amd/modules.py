@@ -364,9 +364,11 @@ class C3k(C3):
 
 class C3k2(C2f):
     """block.py:1064-1084.  With c3k = False and one Bottleneck repeat (the n / s scales' C3k2 at
-    160^2 .. 40^2) the whole block can run as ONE fused kernel (csrc/fused.hip: x read once, the
-    intermediates in LDS, bitwise equal to the four convs).  Opt-in with FCE_FUSE_C3K2=1: measured
-    on MI355X it is still slower than the four tuned convs ("Fused C3k2")."""
+    160^2 .. 40^2) the whole block can run as ONE persistent kernel (csrc/fused.hip: x read once, the
+    intermediates in LDS, bitwise equal to the four convs).  FCE_FUSE_C3K2 (whole-graph lowering):
+    unset / "auto" -- both forms are recorded (fce_net_add_c3k2_alt) and the plan-time autotune keeps the
+    faster per block; "1" -- always the fused kernel (also in the eager drop-in forward); "0" -- never;
+    a number N > 1 -- fused (forced) where h * w <= N."""
 
     def __init__(self, c1, c2, n=1, c3k=False, e=0.5, g=1, shortcut=True):
         super().__init__(c1, c2, n, shortcut, g, e)
@@ -374,13 +376,17 @@ class C3k2(C2f):
             C3k(self.c, self.c, 2, shortcut, g) if c3k else Bottleneck(self.c, self.c, shortcut, g) for _ in range(n)
         )
 
-    def _fused_desc(self, be, x):
+    @staticmethod
+    def _mode() -> str:
         import os
 
-        mode = os.environ.get("FCE_FUSE_C3K2", "0")  # "1": every qualifying block; a number N > 1: h * w <= N
+        return os.environ.get("FCE_FUSE_C3K2", "auto") or "auto"
+
+    def _fused_desc(self, be, x):
+        mode = self._mode()
         if be.shape_only or mode == "0" or not hasattr(be, "c3k2"):
             return None
-        if mode != "1" and x.h * x.w > int(mode):
+        if mode not in ("1", "auto") and x.h * x.w > int(mode):
             return None
         if len(self.m) != 1 or type(self.m[0]) is not Bottleneck or not self.m[0].add:
             return None
@@ -405,6 +411,16 @@ class C3k2(C2f):
         d = self._fused_desc(be, x)
         if d is None:
             return super().emit(be, x, out)
+        if self._mode() == "auto":
+            if not hasattr(be, "c3k2_alt"):  # eager drop-in: the four convs (no plan-time choice there)
+                return super().emit(be, x, out)
+            # both forms: the four convs, then the fused op as their alternative (the plan keeps the faster)
+            first = be.num_ops()
+            y = super().emit(be, x, out)
+            n = be.num_ops() - first
+            if n == 4:
+                be.c3k2_alt(d, x, y, first, n)
+            return y
         y = out if out is not None else be.alloc(x.n, self.cv2.conv.out_channels, x.h, x.w)
         be.c3k2(d, x, y)
         return y

@@ -268,6 +268,16 @@ int fce_net_add_coord(fce_net* net, int kind /*0 BiCoord,1 CoordAtt,2 CoordCross
 int fce_net_add_psa_attention(fce_net* net, int qkv_buf, int heads, int key_dim, int head_dim, const float* pe_w,
                               const float* pe_b, int out_buf, int out_coff);
 int fce_net_add_c3k2(fce_net* net, const fce_c3k2_desc* d, int in_buf, int in_coff, int out_buf, int out_coff);
+/* The fused C3k2 as an ALTERNATIVE to the nops conv ops just added (its cv1, m.cv1, m.cv2, cv2, writing the same
+ * output): exactly one form runs.  The fused form is active until fce_net_plan's autotune times both on the
+ * planned shapes and keeps the faster (FCE_FUSE_C3K2=1: keep the fused form).  Both forms are bitwise equal. */
+int fce_net_add_c3k2_alt(fce_net* net, const fce_c3k2_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
+                         int first_op, int nops);
+/* 1 = op i (an fce_net_add_c3k2_alt op) runs fused, 0 = its convs run, -1 = not such an op */
+int fce_net_c3k2_form(const fce_net* net, int i);
+int fce_net_set_c3k2_form(fce_net* net, int i, int fused);
+/* 1 when op i belongs to the inactive form of an alternative (it launches nothing; profile / op_info report 0) */
+int fce_net_op_skipped(const fce_net* net, int i);
 /* map_bufs[i]: f32 buffer of level i holding cat(box 4*reg_max, cls nc) channels (head.py:122) */
 int fce_net_add_detect(fce_net* net, int nl, const int* map_bufs, const float* strides, int reg_max);
 /* Fused Detect tail conv (see fce_conv2d_detect) writing the forward's pred output; `level` orders

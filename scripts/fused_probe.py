@@ -67,3 +67,29 @@ while i < len(pu) and j < len(pf):
     else:
         i += 1
         j += 1
+
+# the default (auto): both forms recorded, the plan-time autotune's pick per block (tune-log codes 0xF00 / 0xF01)
+import ctypes as C  # noqa: E402
+
+from fce_yolo_amd import _native as N  # noqa: E402
+
+os.environ.pop("FCE_FUSE_C3K2", None)
+ea = Engine(model, a.batch, a.imgsz, dev)
+ya = ea(x).clone()
+torch.cuda.synchronize()
+print(f"auto: bitwise equal to unfused {torch.equal(ya, yu)}")
+k = 0
+op, code, ms = C.c_int(), C.c_int(), C.c_float()
+times = {}
+while N.lib().fce_net_tune_record(ea.be.net, k, C.byref(op), C.byref(code), C.byref(ms)):
+    if code.value & 0xFF0 == 0xF00:
+        times.setdefault(op.value, {})[code.value & 1] = ms.value * 1e3
+    k += 1
+for i in range(ea.num_ops()):
+    f = ea.c3k2_form(i)
+    if f >= 0:
+        t = times.get(i, {})
+        print(f"  op {i}: {'fused' if f else 'convs'} (plan timing: convs {t.get(0, float('nan')):.1f} us, "
+              f"fused {t.get(1, float('nan')):.1f} us)")
+pa = prof(ea)
+print(f"auto forward kernel time {sum(p[3] for p in pa) * 1e3:.1f} us")

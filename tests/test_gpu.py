@@ -66,6 +66,7 @@ def test_op_parity(name, ops_fx, device):
     assert tuple(y.shape) == tuple(ref.shape)
     assert torch.isfinite(y).all()
     err = _rel(y.float(), ref)
+    print(f"OPERR {name} {err:.3e}")
     assert err <= OP_TOL, err
 
 
@@ -231,7 +232,9 @@ def test_full_size_op_parity(key, full_fx, device):
 def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device, monkeypatch):
     """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give, whole-graph
     and per-module; every tile shape the planner picks (8 x 16 on 160^2 maps, 4 x 40 below), forced shapes
-    (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40)."""
+    (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40).  FCE_FUSE_C3K2=1 forces the fused
+    form, =0 records the convs only; the default records both and the plan keeps the faster (auto), and every
+    combination of forms the auto plan can pick is bitwise the same forward."""
     if tile:
         monkeypatch.setenv("FCE_C3K2_TILE", tile)
     model = cases.seeded_model(cfg, 0).to(device)
@@ -241,12 +244,22 @@ def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device,
     names = [eng.op_info(i)[0] for i in range(eng.num_ops())]
     assert "c3k2_fused" in names
     yf = eng(x).clone()
-    monkeypatch.delenv("FCE_FUSE_C3K2")
+    monkeypatch.setenv("FCE_FUSE_C3K2", "0")
     eng2 = Engine(model, batch, imgsz, device)
     assert "c3k2_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
     yu = eng2(x).clone()
     torch.cuda.synchronize()
     assert torch.equal(yf, yu)
+    monkeypatch.delenv("FCE_FUSE_C3K2")
+    ea = Engine(model, batch, imgsz, device)  # auto: both forms recorded, the plan's choice per block
+    alts = [i for i in range(ea.num_ops()) if ea.c3k2_form(i) >= 0]
+    assert alts and ea.num_ops() == eng2.num_ops() + len(alts)
+    assert torch.equal(ea(x).clone(), yu)
+    for fused in (False, True):  # every block in each form (graph replay after the switch re-captures)
+        for i in alts:
+            ea.set_c3k2_form(i, fused)
+        assert all(ea.skipped(j) != fused for i in alts for j in range(i - 4, i))
+        assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
     c3 = next(m for m in model.model if isinstance(m, M.C3k2) and not isinstance(m.m[0], M.C3k))
     xi = torch.randn(batch, c3.cv1.conv.in_channels, 48, 40, device=device).half().contiguous(
         memory_format=torch.channels_last)

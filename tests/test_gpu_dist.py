@@ -67,9 +67,19 @@ def test_sharded_host_predictor_two_ranks_match_one_predictor():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=300) for _ in procs), key=lambda t: t[0])
+    import queue
+    import time
+
+    res, t0 = [], time.time()
+    while len(res) < len(procs):  # a rank that dies fails the test at once instead of leaving the others waiting
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead and time.time() - t0 < 100, f"rank exit codes {[p.exitcode for p in procs]}"
+    res.sort(key=lambda t: t[0])
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
         assert p.exitcode == 0
     pred = Predictor(_model(), TOTAL, S, "cuda:0", lanes=2, conf=0.05)
     want = list(pred.stream(_batches(), return_idxs=True))
