@@ -35,6 +35,7 @@ struct C3Stage {
   const float* b;  // bias (BN folded)
   int cout, cotiles, nsteps, nalloc, fast, cpt, taps;
   int wl;  // 16-byte offset of the stage's fragments in LDS: [cout tile][step][64 lanes]
+  int bl;  // float offset of the stage's bias in the LDS bias block (cotiles * 16, zero past cout)
 };
 
 struct C3k2Args {
@@ -49,6 +50,8 @@ struct C3k2Args {
   int sT, sH, sM;            // LDS strides of the t, h, m images in 16-byte units (odd: conflict-free B reads)
   int oT, oH, oM;            // their 16-byte offsets
   int wtotal;                // 16-byte units of resident fragments
+  int ob, nbias;             // 16-byte offset of the bias block, its floats
+  int diag;                  // FCE_C3K2_DIAG: block 0 prints its per-stage clocks
 };
 
 __device__ __forceinline__ h4 c3_h4(const float (&v)[4]) {
@@ -98,11 +101,13 @@ __device__ __forceinline__ void c3_mma(const h8* wl, int ns, int cot, int c0, in
       if (i < nf && c0 + ct < cot) epi(i, c0 + ct, acc[i][ct]);
 }
 
-// SiLU(acc + bias) of lane group grp's 4 couts of tile ct
-__device__ __forceinline__ void c3_act(const C3Stage& s, int ct, int grp, const f4& acc, float (&v)[4]) {
+// SiLU(acc + bias) of lane group grp's 4 couts of tile ct; the bias from the block's LDS copy (a global load
+// here would make the epilogue wait for the next tile's x prefetch: vmcnt retires in issue order)
+__device__ __forceinline__ void c3_act(const C3Stage& s, const float* bias, int ct, int grp, const f4& acc,
+                                       float (&v)[4]) {
   const int co0 = ct * 16 + grp * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = silu(acc[j] + s.b[co0 + j]);
+  for (int j = 0; j < 4; ++j) v[j] = silu(acc[j] + bias[s.bl + co0 + j]);
 }
 
 // decode tile t of the block's run -> image n, output origin (y0, x0)
@@ -164,10 +169,26 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
       }
     }
   }
+  // biases -> LDS (zero past each conv's cout)
+  float* bias = reinterpret_cast<float*>(sm + a.ob);
+#pragma unroll 1
+  for (int s = 0; s < 4; ++s) {
+    const C3Stage& S = a.st[s];
+    for (int e = int(threadIdx.x); e < S.cotiles * 16; e += NW * 64) bias[S.bl + e] = e < S.cout ? S.b[e] : 0.f;
+  }
   __syncthreads();
 
   const int c8 = a.c / 8;
   const int nfr1 = (a.R2 + 15) >> 4, nfr2 = (a.R1 + 15) >> 4, nfr4 = (a.NC + 15) >> 4;
+  // diagnostics (FCE_C3K2_DIAG=1): block 0, wave 0 sums s_memtime clocks per stage over its tiles and prints them
+  uint64_t clk[6] = {0, 0, 0, 0, 0, 0}, tprev = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+  auto tick = [&](int k) {
+    if (a.diag) {
+      const uint64_t tn = __builtin_amdgcn_s_memtime();
+      clk[k] += tn - tprev;
+      tprev = tn;
+    }
+  };
   _Float16* T = reinterpret_cast<_Float16*>(sm + a.oT);
   _Float16* Hh = reinterpret_cast<_Float16*>(sm + a.oH);
   _Float16* Mm = reinterpret_cast<_Float16*>(sm + a.oM);
@@ -210,9 +231,9 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
             const bool in = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
 #pragma unroll
             for (int ct = 0; ct < MCT; ++ct) {
-              if (c0 + ct >= S.cotiles) continue;
+              if (c0 + ct >= S.cotiles || (c0 + ct) * 16 + grp * 4 >= S.cout) continue;
               float v[4];
-              c3_act(S, c0 + ct, grp, acc[i][ct], v);
+              c3_act(S, bias, c0 + ct, grp, acc[i][ct], v);
               h4 o = c3_h4(v);
               if (!in) o = h4{0, 0, 0, 0};  // the 3x3 convs' zero padding of b
               *reinterpret_cast<h4*>(T + (q * a.sT) * 8 + (c0 + ct) * 16 + grp * 4) = o;
@@ -221,7 +242,9 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         }
       }
     }
+    tick(0);
     if (t + 1 < t_end) c3_load_x<NW, MF1, NS1>(a, t + 1, xb);  // in flight during stages 2-4
+    tick(1);
     __syncthreads();
     // ---------------- stage 2: h = m.cv1(b) over the m.cv1 region (3x3 from the t image)
     {
@@ -258,8 +281,9 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
           if (q >= a.R1) return;
           const int r = q / a.R1W, cq = q - r * a.R1W;
           const int iy = y0 - 1 + r, ix = x0 - 1 + cq;
+          if (ct * 16 + grp * 4 >= S.cout) return;  // partial cout tile (c_mid % 16 == 8)
           float v[4];
-          c3_act(S, ct, grp, acc, v);
+          c3_act(S, bias, ct, grp, acc, v);
           h4 o = c3_h4(v);
           if (!(iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)) o = h4{0, 0, 0, 0};
           *reinterpret_cast<h4*>(Hh + (q * a.sH) * 8 + ct * 16 + grp * 4) = o;
@@ -267,6 +291,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
       }
     }
+    tick(2);
     __syncthreads();
     // ---------------- stage 3: m = m.cv2(h) + b over the tile (3x3 from the h image)
     {
@@ -302,9 +327,10 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
           const int q = (f0 + NW * i) * 16 + col;
           if (q >= a.NC) return;
           const int r = q / a.TW, cq = q - r * a.TW;
-          float v[4];
-          c3_act(S, ct, grp, acc, v);
           const int co0 = ct * 16 + grp * 4;
+          if (co0 >= S.cout) return;  // partial cout tile (c % 16 == 8)
+          float v[4];
+          c3_act(S, bias, ct, grp, acc, v);
           const h4 rv = *reinterpret_cast<const h4*>(T + (((r + 2) * a.R2W + cq + 2) * a.sT) * 8 + a.c + co0);
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
@@ -313,6 +339,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
       }
     }
+    tick(3);
     __syncthreads();
     // ---------------- stage 4: y = cv2([a | b | m]) over the tile, to HBM
     {
@@ -341,16 +368,24 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
           if (q >= a.NC) return;
           const int r = q / a.TW, cq = q - r * a.TW;
           const int iy = y0 + r, ix = x0 + cq;
-          if (iy >= a.H || ix >= a.W) return;
+          if (iy >= a.H || ix >= a.W || ct * 16 + grp * 4 >= S.cout) return;
           float v[4];
-          c3_act(S, ct, grp, acc, v);
+          c3_act(S, bias, ct, grp, acc, v);
           *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + ct * 16 + grp * 4) = c3_h4(v);
         };
         for (int c0 = 0; c0 < S.cotiles; c0 += MCT) c3_mma<MF, MCT>(wl, S.nsteps, S.cotiles, c0, nf, bl, epi);
       }
     }
+    tick(4);
     __syncthreads();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
+    tick(5);
   }
+  if (a.diag && blockIdx.x == 0 && threadIdx.x == 0)
+    printf("c3k2 fused diag: %d tiles, clocks per tile: stage1 %llu, x-issue %llu, stage2 %llu, stage3 %llu, stage4 %llu, "
+           "last barrier %llu\n", t_end - t_begin, (unsigned long long)(clk[0] / (t_end - t_begin)),
+           (unsigned long long)(clk[1] / (t_end - t_begin)), (unsigned long long)(clk[2] / (t_end - t_begin)),
+           (unsigned long long)(clk[3] / (t_end - t_begin)), (unsigned long long)(clk[4] / (t_end - t_begin)),
+           (unsigned long long)(clk[5] / (t_end - t_begin)));
 }
 
 // ============================================================================ host
@@ -380,20 +415,22 @@ static int c3_weights16(const fce_c3k2_desc& d, C3Stage (&st)[4]) {
   const fce_conv_desc m2{d.c_mid, d.c, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
   const fce_conv_desc c2{3 * d.c, d.cout, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
   const fce_conv_desc* cd[4] = {&c1, &m1, &m2, &c2};
-  int off = 0;
+  int off = 0, boff = 0;
   for (int i = 0; i < 4; ++i) {
     st[i] = make_stage(*cd[i], d.w[i], d.b[i]);
     st[i].wl = off;
     off += st[i].cotiles * st[i].nsteps * 64;
+    st[i].bl = boff;
+    boff += st[i].cotiles * 16;
   }
-  return off;
+  return off + boff / 4;  // fragments, then the bias block (16 floats per cout tile = 4 units)
 }
 
 // LDS image of a (TH, TW) tile: t = [a | b] over the cv1 region, h over the m.cv1 region, m over the tile
 static size_t c3_lds(const fce_c3k2_desc& d, int w16, int TH, int TW) {
   const int R2 = (TH + 4) * (TW + 4), R1 = (TH + 2) * (TW + 2), NC = TH * TW;
   const int sT = (2 * d.c / 8) | 1, sH = (d.c_mid / 8) | 1, sM = (d.c / 8) | 1;
-  return size_t(w16 + R2 * sT + R1 * sH + NC * sM) * 16;
+  return size_t(w16 + R2 * sT + R1 * sH + NC * sM) * 16;  // w16: fragments + biases
 }
 
 // tile / waves for a map: 4 waves with two blocks per CU on wide maps, 8 waves and one block per CU
@@ -412,7 +449,14 @@ static bool c3_plan(const fce_c3k2_desc& d, int H, int W, int w16, C3Plan* p) {
       first = 0;
     }
   }
-  for (int i = first; i < nc; ++i) {
+  for (int i = first; i < nc || (nc == 1 && i < 7); ++i) {  // a forced shape that does not fit: the defaults
+    if (nc == 1 && i == 1) {
+      const int dflt[6][3] = {{8, 16, 4}, {4, 40, 8}, {4, 32, 8}, {4, 16, 8}, {2, 40, 8}, {2, 16, 8}};
+      for (int k = 0; k < 6; ++k)
+        for (int j = 0; j < 3; ++j) cand[k][j] = dflt[k][j];
+      i = W >= 128 ? 0 : 1;
+      nc = 6;
+    }
     const int TH = std::min(cand[i][0], H), TW = std::min(cand[i][1], W), NW = cand[i][2];
     const int nfr1 = ((TH + 4) * (TW + 4) + 15) / 16;
     const int mf1 = (nfr1 + NW - 1) / NW;
@@ -425,7 +469,7 @@ static bool c3_plan(const fce_c3k2_desc& d, int H, int W, int w16, C3Plan* p) {
 }
 
 bool c3k2_fused_ok(const fce_c3k2_desc& d) {
-  if (!(d.cin % 32 == 0 && d.cin <= 64 && d.c % 16 == 0 && d.c_mid % 16 == 0 && d.cout % 16 == 0 && 2 * d.c <= 128 &&
+  if (!(d.cin % 32 == 0 && d.cin <= 64 && d.c % 8 == 0 && d.c_mid % 8 == 0 && d.cout % 8 == 0 && 2 * d.c <= 128 &&
         d.c_mid <= 128 && d.cout <= 128))
     return false;
   C3Stage st[4];
@@ -490,6 +534,12 @@ int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y,
   a.sH = (d.c_mid / 8) | 1;
   a.sM = (d.c / 8) | 1;
   a.wtotal = w16;
+  a.ob = a.st[3].wl + a.st[3].cotiles * a.st[3].nsteps * 64;  // the bias block follows the fragments
+  a.nbias = (w16 - a.ob) * 4;
+  {
+    const char* de = getenv("FCE_C3K2_DIAG");
+    a.diag = de && atoi(de) != 0;
+  }
   a.oT = w16;
   a.oH = a.oT + a.R2 * a.sT;
   a.oM = a.oH + a.R1 * a.sH;

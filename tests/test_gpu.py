@@ -258,7 +258,8 @@ def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device,
     for fused in (False, True):  # every block in each form (graph replay after the switch re-captures)
         for i in alts:
             ea.set_c3k2_form(i, fused)
-        assert all(ea.skipped(j) != fused for i in alts for j in range(i - 4, i))
+        assert all(ea.skipped(j) == fused for i in alts for j in range(i - 4, i)) and all(ea.skipped(i) != fused
+                                                                                          for i in alts)
         assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
     c3 = next(m for m in model.model if isinstance(m, M.C3k2) and not isinstance(m.m[0], M.C3k))
     xi = torch.randn(batch, c3.cv1.conv.in_channels, 48, 40, device=device).half().contiguous(
