@@ -50,10 +50,12 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+        tmp = LIB.with_suffix(".so.tmp")  # linked aside, then renamed: the library is never seen half-written
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
     return LIB
 
 

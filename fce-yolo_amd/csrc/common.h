@@ -65,7 +65,17 @@ LaunchProbe*& probe_slot();  // thread-local slot (api.hip)
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------- device math
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) in place of IEEE division: the division
+// expands to ~10 VALU ops (scale / rcp / 4 fma / fmas / fixup) and the conv epilogues are VALU-heavy
+// (a 1x1 conv with cin 64 spends more SIMD cycles on its epilogue than on its MFMAs).  Every kernel
+// uses this one definition, so the variants stay bitwise identical to each other.  The product is kept out of
+// FMA contraction (the pragma): unlike a quotient, hipcc fuses it with a following add (a residual: one v_fma,
+// one rounding) in some kernels and not in others.  (An fpin here would also do, but it cannot be speculated:
+// every `act ? silu(t) : t` becomes a branch per element.)
+__device__ __forceinline__ float silu(float x) {
+#pragma clang fp contract(off)
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
 // An fp32 value pinned in a register.  Without it hipcc fuses a multiply or add with the fp16
 // conversion that follows (v_fma_mix*: one rounding instead of two) in some kernels and not in
 // others, and conv variants that must be bitwise identical differ in the last fp16 bit.
@@ -73,7 +83,7 @@ __device__ __forceinline__ float fpin(float x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // BiFPN normalised weight (fce_block.py:57-58): relu(w_i) / (sum_j relu(w_j) + 1e-4)
 __device__ __forceinline__ float fusion_alpha(const float* w, int n, int i) {

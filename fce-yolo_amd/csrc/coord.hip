@@ -39,7 +39,10 @@ static size_t align_f(size_t n) { return (n + 63) & ~size_t(63); }
 // second launch costs more (n L5 58.5 vs 62.0 us per call; l L5 256 -> 252, m L5 434.5 -> 422.6, r03r)
 static constexpr int kBandMaxK = 8;  // columns per thread: W <= 32 * kBandMaxK
 static bool band_pool_ok(int C, int W) { return C >= 256 && C % 64 == 0 && W <= 32 * kBandMaxK; }
-static int band_rows(int N, int H, int C) { return int64_t(N) * ((H + 15) / 16) * (C / 64) >= 512 ? 16 : 8; }
+// Rows per pooling band: fixed.  The column means add the bands' partial sums, so the band height sets the
+// summation order; a height chosen by batch size (8 rows below 512 blocks, as before) made an image's pooled
+// columns depend on its batch whenever the fp32 sums were inexact (test_batch_invariance, m-h8 1280 bs16).
+static int band_rows(int, int, int) { return 16; }
 
 static size_t ws_layout(const fce_coord_desc& d, int n, int h, int w, CoordWs* out, float* base) {
   const int L = h > w ? h : w;

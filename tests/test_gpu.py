@@ -2,7 +2,9 @@
 oracle; end-to-end detection outputs; bit-exact NMS indices; graph/eager/batch invariance.
 
 Tolerances (fp16 storage, fp32 accumulate, fp32 decode — Q11):
-  * per op:        max|ours - ref| <= OP_TOL * max|ref|           (OP_TOL = 4e-3)
+  * per op:        max|ours - ref| <= OP_TOL * max|ref|           (OP_TOL = 1e-3: every op fixture, the full-size
+                   BiCoord / C2PSA fixtures included, measures 2.9e-4 .. 8.0e-4 on MI355X; fp16 storage rounds
+                   at 2^-11 = 4.9e-4 of max|ref|, so 1e-3 is two fp16 half-ulps of headroom)
   * end-to-end:    boxes  max|d xywh| <= 1e-3 * max|xywh|   (north-star "1e-3 fp16 tolerance", relative)
                    scores max|d sigmoid| <= 1e-3               (absolute, scores in [0, 1])
   * NMS:           kept anchor indices and (k, 6) rows bit-exact vs the reference on the same preds.
@@ -23,7 +25,7 @@ from fce_yolo_amd.engine import NMS, Engine, Pipeline, non_max_suppression
 from oracle import nms_oracle
 
 pytestmark = pytest.mark.gpu
-OP_TOL = 4e-3
+OP_TOL = 1e-3
 BOX_TOL = 1e-3
 CLS_TOL = 1e-3
 
@@ -721,7 +723,9 @@ def test_conv1x1_variants_views_and_upsampling(cin, cout, up, xpad, ypad, epi, d
     base = outs[-1]
     for code, y in outs.items():
         assert torch.equal(y, base), (hex(code), (y.float() - base.float()).abs().max().item())
-    assert _rel(base, ref) <= 4e-3
+    err = _rel(base, ref)
+    print(f"OPERR variants {err:.3e}")
+    assert err <= OP_TOL, err
     if epi != N.EPI_STORE:
         return
     # the duplicate store (C2f / C3k2 cv1, fce_net_add_conv_dup) through every variant's store path: the dense
@@ -777,7 +781,9 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     base = outs[-1]
     for code, y in outs.items():
         assert torch.equal(y, base), hex(code)
-    assert _rel(base, ref) <= 4e-3
+    err = _rel(base, ref)
+    print(f"OPERR variants {err:.3e}")
+    assert err <= OP_TOL, err
 
 
 @pytest.mark.parametrize("c,stride,H,W,cpad", [
@@ -815,11 +821,13 @@ def test_dwconv_every_variant_bitwise_and_parity(c, stride, H, W, cpad, device):
     base = outs[-1]
     for code, y in outs.items():
         assert torch.equal(y, base), (code, (y.float() - base.float()).abs().max().item())
-    assert _rel(base, ref) <= 4e-3
+    err = _rel(base, ref)
+    print(f"OPERR variants {err:.3e}")
+    assert err <= OP_TOL, err
 
 
 @pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11s-bifpn.yaml", 2, 256),
-                                             ("yolo11n-fce.yaml", 1, 640)])
+                                             ("yolo11n-fce.yaml", 1, 640), ("yolo11m-fce.yaml", 1, 320)])
 def test_every_op_variant_bitwise_in_model(cfg, batch, imgsz, device, monkeypatch):
     """Each conv op of a planned model, pinned in turn to every candidate kernel variant, leaves the
     whole forward bitwise unchanged (the model's own views, upsampling, BiFPN / Detect epilogues and
