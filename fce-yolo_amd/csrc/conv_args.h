@@ -141,7 +141,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         float den = 0.f, num = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float e = expf(v[j] - mx);
+          const float e = __expf(v[j] - mx);  // v_exp_f32 (as detect_decode)
           den += e;
           num = __fadd_rn(num, __fmul_rn(e, (float)(grp * 4 + j)));  // no FMA: match detect_decode
         }
@@ -185,7 +185,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (co0 + j < a.cout) {
-            const float sc = 1.0f / (1.0f + expf(-(acc[r][p][j] + a.bias[co0 + j])));
+            const float sc = sigmoidf_(acc[r][p][j] + a.bias[co0 + j]);
             o[int64_t(co0 + j) * a.det_A] = sc;
             const unsigned long long key =
                 (uint64_t(__float_as_uint(sc)) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(co0 + j));

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs a) {
           sd[g] = 0.f;
           sn[g] = 0.f;
           for (int j = 0; j < 4; ++j) {
-            const float e = expf(b[g * 4 + j] - mx);
+            const float e = __expf(b[g * 4 + j] - mx);
             sd[g] += e;
             sn[g] = __fadd_rn(sn[g], __fmul_rn(e, (float)(g * 4 + j)));  // no FMA: match the fused path
           }
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs a) {
         num = (sn[0] + sn[1]) + (sn[2] + sn[3]);
       } else {
         for (int i = 0; i < a.reg_max; ++i) {
-          const float e = expf(b[i] - mx);
+          const float e = __expf(b[i] - mx);
           den += e;
           num += e * (float)i;
         }
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void detect_decode_kernel(DecodeArgs a) {
     o[int64_t(2) * a.A] = (x2 - x1) * L.stride;
     o[int64_t(3) * a.A] = (y2 - y1) * L.stride;
     const float* cl = L.cls + (int64_t(n) * L.h * L.w + p) * L.ccs;
-    for (int c = 0; c < a.nc; ++c) o[int64_t(4 + c) * a.A] = 1.0f / (1.0f + expf(-cl[c]));
+    for (int c = 0; c < a.nc; ++c) o[int64_t(4 + c) * a.A] = sigmoidf_(cl[c]);
   }
 }
 

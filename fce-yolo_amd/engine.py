@@ -11,6 +11,7 @@ max_nms 30000, max_wh 7680) and returns the same per-image (k, 6) tensors and ke
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -277,6 +278,9 @@ class Pipeline:
         self.used = [False] * depth
         self.pending = None  # slot whose NMS is not issued yet (defer)
         self.i = 0
+        # diagnostics only (FCE_PIPE_SKIP_NMS=1): lanes run the forwards alone, so the NMS's share of the pipelined
+        # step can be measured; the results are then meaningless
+        self._skip_nms = os.environ.get("FCE_PIPE_SKIP_NMS") == "1"
         if defer:
             N.call("fce_net_set_fork", engine.net, N.lib().fce_net_fork_hint(engine.net))
 
@@ -302,7 +306,8 @@ class Pipeline:
         with torch.cuda.stream(s):
             eng(x, out=self.preds[k], best=self.bests[k])
             self.fwd_done[k].record(s)
-            self.nms[k](self.preds[k], self.bests[k])
+            if not self._skip_nms:
+                self.nms[k](self.preds[k], self.bests[k])
             self.lane_done[k].record(s)
         if self.post is None:
             self.nms_done[k] = self.lane_done[k]
