@@ -76,6 +76,12 @@ __device__ __forceinline__ float silu(float x) {
 #pragma clang fp contract(off)
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
+// bias[co] for co < n, else 0, with the load unconditional (index clamped): a load under a branch makes hipcc wait
+// for it with vmcnt(0), which on CDNA4 also waits for every store the epilogue has issued before it
+__device__ __forceinline__ float bias_or0(const float* b, int co, int n) {
+  const float v = b[co < n ? co : n - 1];
+  return co < n ? v : 0.f;
+}
 // An fp32 value pinned in a register.  Without it hipcc fuses a multiply or add with the fp16
 // conversion that follows (v_fma_mix*: one rounding instead of two) in some kernels and not in
 // others, and conv variants that must be bitwise identical differ in the last fp16 bit.

@@ -399,7 +399,7 @@ __device__ __forceinline__ void conv_store_staged(const ConvArgs& a, f4 (&acc)[R
     if (cbl0 + ctl >= cotiles) continue;
     float bz[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bz[j] = bias_or0(a.bias, co0 + j, a.cout);
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       const int px = pw + p * 16 + col, pix = pix0 + px;
@@ -1332,47 +1332,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RP; ++p) acc[r][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], bf[p], acc[r][p], 0, 0, 0);
   }
-  // epilogue: bias, SiLU, optional residual, fp16 NHWC store
-  const int ox = ox0 + col;
-  if (ox >= a.Wo) return;
-#pragma unroll
-  for (int r = 0; r < RC; ++r) {
-    const int co0 = (cot0 + r) * 16 + grp * 4;
-    if (cot0 + r >= cotiles || co0 >= a.cout) continue;
-    float bz[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
-#pragma unroll
-    for (int p = 0; p < RP; ++p) {
-      const int oy = oy0 + wave * RP + p;
-      if (oy >= a.Ho) continue;
-      const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float tt = acc[r][p][j] + bz[j];
-        v[j] = a.act ? silu(tt) : tt;
-      }
-      _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
-      if (a.res) {
-        const _Float16* ro = a.res + pix * a.rcs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          const h4 rv = *reinterpret_cast<const h4*>(ro);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
-        } else {
-          for (int j = 0; j < 4; ++j)
-            if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
-        }
-      }
-      if (a.vec_ok && co0 + 3 < a.cout) {
-        *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
-      } else {
-        for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
-      }
-    }
-  }
+  tile3_store<RC, RP>(a, acc, n, oy0 + wave * RP, ox0, cot0, col, grp);  // bias, SiLU, residual, fp16 store
 }
 
 static size_t small_tile_lds(int stride, int rp, int cin) {
@@ -1593,8 +1553,8 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
 // Column-run variant: thread = (output column ox, 8-channel group), consecutive lanes = consecutive
 // channel groups then columns, so every load / store instruction covers contiguous pixels (full
 // lines); each thread computes PY outputs down its column from (PY-1)*S+3 input rows, every loaded
-// row feeding all the outputs that use it.  Out-of-image taps are skipped (selects, no branches) and
-// each output accumulates its taps in (ky, kx) order with fmaf, like the other variants.
+// row feeding all the outputs that use it.  Out-of-image taps load the zero line and add fmaf(0, w, acc) == acc,
+// the value the other variants get by skipping them; each output accumulates its taps in (ky, kx) order with fmaf.
 template <int S, int PY>
 __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
   const int cg = a.C >> 3;
@@ -1647,15 +1607,12 @@ __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
     for (int p = 0; p < PY; ++p) {
       const int ky = r - p * S;
       if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
+      // an out-of-image tap loaded the zero line: fmaf(0, w, acc) == acc (the skipped tap of the other variants;
+      // a select per FMA here was a third of the kernel's VALU work)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const bool ok = rin && cok[kx];
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = __builtin_fmaf((float)v[kx][j], wk[ky * 3 + kx][j], acc[p][j]);
-          acc[p][j] = ok ? f : acc[p][j];
-        }
-      }
+        for (int j = 0; j < 8; ++j) acc[p][j] = __builtin_fmaf((float)v[kx][j], wk[ky * 3 + kx][j], acc[p][j]);
     }
   }
 #pragma unroll
@@ -1818,7 +1775,7 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int co = co0 + j;
-        const float t = acc[co] + (co < a.cout ? a.bias[co] : 0.f);
+        const float t = acc[co] + bias_or0(a.bias, co, a.cout);
         o[j] = (_Float16)(a.act ? silu(t) : t);
       }
       *reinterpret_cast<h8*>(yo + co0) = o;
@@ -1940,7 +1897,7 @@ __global__ __launch_bounds__(256) void stem_s2_kernel(StemArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int co = c8 * 8 + e;
-        const float t = acc[j][co] + (co < a.cout ? a.bias[co] : 0.f);
+        const float t = acc[j][co] + bias_or0(a.bias, co, a.cout);
         o[j][c8][e] = (_Float16)(a.act ? silu(t) : t);
       }
   if (a.cout == COUT && a.ycs == COUT) {
@@ -2003,10 +1960,20 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float
     if (ne <= NLS * 256) {
       h8 v[NLS];
       int dst[NLS];
+      // (staged row, chunk) of e = threadIdx.x + 256 i, stepped without a division per chunk
+      const int dq = 256 % CW, dcr = 256 / CW;
+      int cr = int(threadIdx.x) / CW, q = int(threadIdx.x) - cr * CW;
 #pragma unroll
       for (int i = 0; i < NLS; ++i) {
         const int e = threadIdx.x + 256 * i;
-        const int cr = e / CW, q = e - cr * CW;
+        if (i > 0) {
+          q += dq;
+          cr += dcr;
+          if (q >= CW) {
+            q -= CW;
+            ++cr;
+          }
+        }
         const int ci = cr / IR, r = cr - ci * IR;
         const int iy = 2 * oy0 - 1 + r, ix0 = (q - 1) * 8;
         const bool ok = e < ne && iy >= 0 && iy < a.H && q >= 1 && ix0 < a.W;
@@ -2043,14 +2010,14 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float
       *reinterpret_cast<h8*>(ssm + cr * WP + q * 8) = v;
     }
   }
-  // this lane's 8 k values: (ci, ky, kx) -> LDS offset relative to the pixel's window origin
+  // this lane's 8 k values: (ci, ky, kx) -> LDS offset relative to the pixel's window origin.  k >= cin * 9 (the
+  // zero-padded tail of the K-step) reads tap (0, 0, 0) again: its weights are zero and the value finite
+  // (that tap is also a real tap of the same output), so the gather needs no per-element select or exec mask
   int koff[8];
-  bool kin[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int kq = 8 * grp + j, ci = kq / 9, t = kq - ci * 9;
-    kin[j] = kq < a.C * 9;
-    koff[j] = kin[j] ? (ci * IR + t / 3) * WP + (t % 3) : 0;  // staged col of ix = 2 ox - 1 + kx is 2 ox + 7 + kx
+    koff[j] = kq < a.C * 9 ? (ci * IR + t / 3) * WP + (t % 3) : 0;  // staged col of ix = 2 ox - 1 + kx is 2 ox + 7 + kx
   }
   h8 af[RC];
 #pragma unroll
@@ -2061,32 +2028,35 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a, const _Float
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int co = r * 16 + grp * 4 + j;
-      bz[r][j] = co < a.cout ? a.bias[co] : 0.f;
+      bz[r][j] = bias_or0(a.bias, co, a.cout);
     }
   __syncthreads();
+  // the block's outputs: rows oy0 .. oy0 + SR - 1 of image n; 32-bit offsets from the block's first pixel
+  _Float16* yb = a.y + (int64_t(n) * a.Ho + oy0) * a.Wo * a.ycs;
   const int fpr = (a.Wo + 15) / 16;  // fragments per output row
-  for (int f = wave; f < SR * fpr; f += 4) {
-    const int rr = f / fpr, fx = f - rr * fpr;
-    const int oy = oy0 + rr;
-    if (oy >= a.Ho) break;
-    const int ox = fx * 16 + col;
-    const int base = (2 * rr) * WP + 2 * min(ox, a.Wo - 1) + 7;  // window origin: staged row 2 rr, col 2 ox + 7
-    h8 b;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = kin[j] ? ssm[base + koff[j]] : (_Float16)0.f;
-    _Float16* yo = a.y + ((int64_t(n) * a.Ho + oy) * a.Wo + ox) * a.ycs;
+  for (int rr = 0; rr < SR; ++rr) {
+    if (oy0 + rr >= a.Ho) break;
+    for (int fx = wave; fx < fpr; fx += 4) {
+      const int ox = fx * 16 + col;
+      const int base = (2 * rr) * WP + 2 * min(ox, a.Wo - 1) + 7;  // window origin: staged row 2 rr, col 2 ox + 7
+      h8 b;
 #pragma unroll
-    for (int r = 0; r < RC; ++r) {
-      const f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], b, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const int co0 = r * 16 + grp * 4;
-      if (ox < a.Wo && co0 < a.cout) {
-        h4 o;
+      for (int j = 0; j < 8; ++j) b[j] = ssm[base + koff[j]];
+      _Float16* yo = yb + (rr * a.Wo + ox) * a.ycs;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float t = d[j] + bz[r][j];
-          o[j] = (_Float16)(a.act ? silu(t) : t);
+      for (int r = 0; r < RC; ++r) {
+        const f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r], b, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int co0 = r * 16 + grp * 4;
+        if (ox < a.Wo && co0 < a.cout) {
+          h4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float t = d[j] + bz[r][j];
+            o[j] = (_Float16)(a.act ? silu(t) : t);
+          }
+          *reinterpret_cast<h4*>(yo + co0) = o;
         }
-        *reinterpret_cast<h4*>(yo + co0) = o;
       }
     }
   }

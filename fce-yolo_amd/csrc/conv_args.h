@@ -74,13 +74,36 @@ __device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP]
   const int cotiles = (a.cout + 15) >> 4;
   const int ox = ox0 + col;
   if (ox >= a.Wo) return;
+  // residuals of RG cout tiles x RP rows loaded before their first store (see conv_epilogue)
+  constexpr int RG = RC * RP <= 8 ? RC : 1;
+  const bool vres = a.res && a.vec_ok && a.cout >= 4;
 #pragma unroll
-  for (int r = 0; r < RC; ++r) {
+  for (int r0 = 0; r0 < RC; r0 += RG) {
+    h4 rpre[RG][RP];
+    if (vres) {
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        const int co0 = min((cot0 + r0 + g) * 16 + grp * 4, (a.cout - 4) & ~3);
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int64_t pix = (int64_t(n) * a.Ho + min(oy0 + p, a.Ho - 1)) * a.Wo + ox;
+          rpre[g][p] = *reinterpret_cast<const h4*>(a.res + pix * a.rcs + co0);
+        }
+      }
+      // all of them landed before the first store: hipcc otherwise waits vmcnt(0) at every join of the store loop
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int r = r0 + g;
     const int co0 = (cot0 + r) * 16 + grp * 4;
     if (cot0 + r >= cotiles || co0 >= a.cout) continue;
     float bz[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bz[j] = bias_or0(a.bias, co0 + j, a.cout);
+    // landed before the stores: with a load still pending at the joins of the loop below hipcc waits vmcnt(0),
+    // i.e. also for the previous row's store, at every row
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       const int oy = oy0 + p;
@@ -93,24 +116,26 @@ __device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP]
         v[j] = a.act ? silu(tt) : tt;
       }
       _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
+      const bool vec = a.vec_ok && co0 + 3 < a.cout;
       if (a.res) {
-        const _Float16* ro = a.res + pix * a.rcs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          const h4 rv = *reinterpret_cast<const h4*>(ro);
+        if (vec) {
+          const h4 rv = rpre[g][p];
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
         } else {
+          const _Float16* ro = a.res + pix * a.rcs + co0;
           for (int j = 0; j < 4; ++j)
             if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
         }
       }
-      if (a.vec_ok && co0 + 3 < a.cout) {
+      if (vec) {
         *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
       } else {
         for (int j = 0; j < 4; ++j)
           if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
       }
     }
+  }
   }
 }
 
@@ -125,6 +150,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
     // Detect box branch (head.py:161-162, block.py:76-79, tal.py:367-376): the 4 x 16 logits of a
     // pixel live in tiles r = side, lanes {p, p+16, p+32, p+48} x 4 registers -> softmax expectation
     // with two xor-shuffles, then xywh * stride into pred rows 0..3 (fp32 throughout).
+    float bz[4][4];  // loaded once, not per pixel
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bz[r][j] = a.bias[r * 16 + grp * 4 + j];
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       float dist[4];
@@ -133,7 +163,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         float v[4], mx = -INFINITY;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[j] = acc[r < RC ? r : 0][p][j] + a.bias[r * 16 + grp * 4 + j];
+          v[j] = acc[r < RC ? r : 0][p][j] + bz[r][j];
           mx = fmaxf(mx, v[j]);
         }
         mx = fmaxf(mx, __shfl_xor(mx, 16));
@@ -169,24 +199,41 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
   if (OUT == OUT_CLS) {  // Detect cls branch: sigmoid(logit) into pred rows 4..
     // with det_best: the pixel's best class over this wave's couts (first maximum, like torch.max in
     // utils/nms.py) as one key = score bits << 32 | ~class (scores >= 0: integer order = float order;
-    // ties -> the lower class), merged over the 4 cout groups by xor-shuffles, one atomic max per pixel
+    // ties -> the lower class), merged over the 4 cout groups by xor-shuffles, one atomic max per pixel.
+    // The biases are loaded once per cout tile and the pixel's pred column once per pixel: loaded per element
+    // (as before) every score waited for its own bias load, and the epilogue was the kernel's bound.
     unsigned long long bk[RP];
+    float* orow[RP];  // pred[n][4][a0 + q] of this lane's pixels (nullptr: past the end)
 #pragma unroll
-    for (int p = 0; p < RP; ++p) bk[p] = 0ull;
+    for (int p = 0; p < RP; ++p) {
+      bk[p] = 0ull;
+      const int pix = pix_base + p * 16 + col;
+      const int n = pix / a.det_hw, q = pix - n * a.det_hw;
+      orow[p] = pix < a.P ? a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q : nullptr;
+    }
+    // every bias of the wave's couts loaded (unconditionally: clamped) and landed before the first score store:
+    // a load issued after a store, or pending at a join, is waited for with vmcnt(0), i.e. with every store
+    float bzr[RC][4];
+#pragma unroll
+    for (int r = 0; r < RC; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bzr[r][j] = a.bias[min((cot0 + r) * 16 + grp * 4 + j, a.cout - 1)];
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
     for (int r = 0; r < RC; ++r) {
       const int co0 = (cot0 + r) * 16 + grp * 4;
+      const float* bz = bzr[r];
+      const int64_t rofs = int64_t(co0) * a.det_A;
+      const int nv = min(4, a.cout - co0);  // valid couts of this lane group (<= 0: none)
 #pragma unroll
       for (int p = 0; p < RP; ++p) {
-        const int pix = pix_base + p * 16 + col;
-        if (pix >= a.P) continue;
-        const int n = pix / a.det_hw, q = pix - n * a.det_hw;
-        float* o = a.pred + (int64_t(n) * (4 + a.det_nc) + 4) * a.det_A + a.det_a0 + q;
+        if (!orow[p]) continue;
+        float* o = orow[p] + rofs;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (co0 + j < a.cout) {
-            const float sc = sigmoidf_(acc[r][p][j] + a.bias[co0 + j]);
-            o[int64_t(co0 + j) * a.det_A] = sc;
+          if (j < nv) {
+            const float sc = sigmoidf_(acc[r][p][j] + bz[j]);
+            o[int64_t(j) * a.det_A] = sc;
             const unsigned long long key =
                 (uint64_t(__float_as_uint(sc)) << 32) | uint64_t(0xFFFFFFFFu - uint32_t(co0 + j));
             bk[p] = key > bk[p] ? key : bk[p];
@@ -212,13 +259,37 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
   }
   float alpha = 1.f;
   if (OUT == OUT_WSTORE || OUT == OUT_ACCUM) alpha = fusion_alpha(a.fw, a.fn, a.fi);
+  // The vector path's residual (and the ACCUM target) of RG cout tiles x RP pixels are loaded before the first of
+  // their stores: a load issued after a store is waited for together with that store (CDNA4 vmcnt counts stores),
+  // which serialised every (tile, pixel) of the epilogue on a store round trip.  Clamped addresses: the loads are
+  // unconditional inside one uniform branch; lanes past the edge use the scalar path below, as before.
+  constexpr int RG = RC * RP <= 8 ? RC : 1;
+  const bool vres = a.res && a.vec_ok && a.cout >= 4, vacc = OUT == OUT_ACCUM && a.vec_ok && a.cout >= 4;
 #pragma unroll
-  for (int r = 0; r < RC; ++r) {
+  for (int r0 = 0; r0 < RC; r0 += RG) {
+    h4 rpre[RG][RP], apre[RG][RP];
+    if (OUT != OUT_F32 && (vres || vacc)) {
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        const int co0 = min((cot0 + r0 + g) * 16 + grp * 4, (a.cout - 4) & ~3);  // 8-byte aligned, in range
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int pix = min(pix_base + p * 16 + col, a.P - 1);
+          if (vres) rpre[g][p] = *reinterpret_cast<const h4*>(a.res + int64_t(pix) * a.rcs + co0);
+          if (vacc) apre[g][p] = *reinterpret_cast<const h4*>(static_cast<const _Float16*>(a.y) + int64_t(pix) * a.ycs + co0);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): all landed before the first store (tile3_store)
+    }
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int r = r0 + g;
     const int co0 = (cot0 + r) * 16 + grp * 4;
     if (cot0 + r >= cotiles || co0 >= a.cout) continue;
     float bz[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bz[j] = bias_or0(a.bias, co0 + j, a.cout);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) before the stores (tile3_store)
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       const int pix = pix_base + p * 16 + col;
@@ -240,13 +311,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         continue;
       }
       _Float16* yo = static_cast<_Float16*>(a.y) + int64_t(pix) * a.ycs + co0;
+      const bool vec = a.vec_ok && co0 + 3 < a.cout;
       if (a.res) {
-        const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
-        if (a.vec_ok && co0 + 3 < a.cout) {
-          h4 rv = *reinterpret_cast<const h4*>(ro);
+        if (vec) {
+          const h4 rv = rpre[g][p];
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
         } else {
+          const _Float16* ro = a.res + int64_t(pix) * a.rcs + co0;
           for (int j = 0; j < 4; ++j)
             if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
         }
@@ -255,9 +327,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha);
       }
-      if (a.vec_ok && co0 + 3 < a.cout) {
+      if (vec) {
         if (OUT == OUT_ACCUM) {
-          h4 pv4 = *reinterpret_cast<const h4*>(yo);
+          const h4 pv4 = apre[g][p];
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin((float)pv4[j] + fpin(alpha * v[j]));
         }
@@ -276,6 +348,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f4 (&acc)[RC][R
         }
       }
     }
+  }
   }
 }
 

@@ -46,7 +46,7 @@ __device__ __forceinline__ void big1_store_staged(const ConvArgs& a, f4 (&acc)[W
     if (cbl0 + ctl >= cotiles) continue;
     float bz[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = (co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bz[j] = bias_or0(a.bias, co0 + j, a.cout);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int px = wp * 64 + p * 16 + col, pix = p0 + px;

@@ -921,7 +921,7 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
     for (int j = 0; j < 8; ++j) {
       float r;
       if (MODE == GATE_BICOORD)
-        r = (float)v[k][j] * (1.0f / (1.0f + __expf(-(gv[j] + wv[j]))));
+        r = (float)v[k][j] * sigmoidf_(gv[j] + wv[j]);  // v_exp + v_rcp (the gate is VALU-bound)
       else if (MODE == GATE_COORD)
         r = (float)v[k][j] * gv[j] * wv[j];
       else

@@ -11,4 +11,7 @@ timeout -s KILL 120 rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d g
   python scripts/pmc_kernel.py > gpurun_out/$TAG/valu.log 2>&1
 rc=$?; echo "valu pass rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python scripts/pmc_by_kernel.py gpurun_out/$TAG/valu > gpurun_out/$TAG/valu_by_kernel.txt
+rc=$?
+NL=$(grep -o "launches per forward [0-9]*" gpurun_out/$TAG/valu.log | grep -o "[0-9]*$")
+[ $rc -eq 0 ] && python scripts/pmc_last_forward.py gpurun_out/$TAG/valu $NL > gpurun_out/$TAG/valu_last_forward.txt
 rc=$?; rm -rf gpurun_out/$TAG/valu; exit $rc

@@ -18,6 +18,7 @@ model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_di
 model.eval().to(dev)
 x = torch.rand(32, 3, 640, 640, generator=torch.Generator().manual_seed(1000)).half().to(dev)
 eng = Engine(model, 32, 640, dev)
+print("launches per forward", sum(q[4] for q in eng.profile(x, launches=True)), flush=True)
 for _ in range(3):
     eng(x)
 torch.cuda.synchronize()
