@@ -368,29 +368,82 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
     base += s_total;
     __syncthreads();
   }
-  for (int a0 = 0; !multi && a0 < A; a0 += NMS_THREADS) {
-    const int a = a0 + threadIdx.x;
-    float best = -INFINITY;
-    int bj = 0;
-    if (a < A) {
-      if (bestk) {  // fused into the Detect cls epilogue: score bits << 32 | ~class
-        const unsigned long long k = bestk[int64_t(n) * A + a];
-        best = __uint_as_float(uint32_t(k >> 32));
-        bj = int(0xFFFFFFFFu - uint32_t(k));
-      } else {
-        best = w.aconf[a];
-        bj = w.acls[a];
+  // best-class candidates: groups of CG chunks of 1024 anchors, ONE scan per group (two barriers) over the
+  // per-(chunk, wave) counts, instead of a block scan (three barriers) per chunk; the candidates' box loads of
+  // the whole group are issued before any of its workspace writes.  Same positions: anchor order.
+  constexpr int CG = 9;
+  __shared__ int gcnt[CG * NWAVES];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int g0 = 0; !multi && g0 < A; g0 += CG * NMS_THREADS) {
+    float best[CG];
+    int bj[CG];
+    uint32_t fl = 0;
+#pragma unroll
+    for (int c = 0; c < CG; ++c) {
+      const int a = g0 + c * NMS_THREADS + int(threadIdx.x);
+      best[c] = -INFINITY;
+      bj[c] = 0;
+      if (a < A) {
+        if (bestk) {  // fused into the Detect cls epilogue: score bits << 32 | ~class
+          const unsigned long long k = bestk[int64_t(n) * A + a];
+          best[c] = __uint_as_float(uint32_t(k >> 32));
+          bj[c] = int(0xFFFFFFFFu - uint32_t(k));
+        } else {
+          best[c] = w.aconf[a];
+          bj[c] = w.acls[a];
+        }
+      }
+      const bool f = a < A && best[c] > conf_thres && allowed(bj[c]);
+      fl |= uint32_t(f) << c;
+      const uint64_t m = __ballot(f);
+      if (lane == 0) gcnt[c * NWAVES + wv] = __popcll(m);
+    }
+    __syncthreads();
+    if (wv == 0) {  // exclusive prefix over (chunk, wave) = anchor order, offset by the candidates so far
+      constexpr int PER = (CG * NWAVES + 63) / 64;
+      int v[PER], sum = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = lane * PER + k;
+        v[k] = idx < CG * NWAVES ? gcnt[idx] : 0;
+        sum += v[k];
+      }
+      int inc = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      int ex = base + inc - sum;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = lane * PER + k;
+        if (idx < CG * NWAVES) gcnt[idx] = ex;
+        ex += v[k];
+      }
+      if (lane == 63) s_total = base + inc;
+    }
+    __syncthreads();
+    float cx[CG], cy[CG], hw[CG], hh[CG];
+#pragma unroll
+    for (int c = 0; c < CG; ++c) {
+      const int a = g0 + c * NMS_THREADS + int(threadIdx.x);
+      if ((fl >> c) & 1u) {
+        cx[c] = P[a];
+        cy[c] = P[int64_t(1) * A + a];
+        hw[c] = P[int64_t(2) * A + a] / 2.0f;
+        hh[c] = P[int64_t(3) * A + a] / 2.0f;
       }
     }
-    const int flag = (a < A) && (best > conf_thres) && allowed(bj);
-    const int pos = block_scan(flag, wsum, &s_total);
-    if (flag) {
-      const float cx = P[a], cy = P[int64_t(1) * A + a];
-      const float hw = P[int64_t(2) * A + a] / 2.0f, hh = P[int64_t(3) * A + a] / 2.0f;
-      put(base + pos, a, best, bj, cx, cy, hw, hh);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) {
+      const bool f = (fl >> c) & 1u;
+      const uint64_t m = __ballot(f);
+      if (f) put(gcnt[c * NWAVES + wv] + __popcll(m & lt), g0 + c * NMS_THREADS + int(threadIdx.x), best[c], bj[c],
+                 cx[c], cy[c], hw[c], hh[c]);
     }
-    base += s_total;
-    __syncthreads();
+    base = s_total;
+    __syncthreads();  // gcnt / s_total are rewritten by the next group
   }
   const int ncand = base;
   degenerate = __syncthreads_or(degenerate);
