@@ -1261,14 +1261,17 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
 // tap = c / cpt): the same A fragments and the same per-output summation order as conv_mfma_kernel, so
 // the two give bitwise-identical results.  Input pixels are read from HBM once (plus halo) instead of
 // once per tap from L2.
-template <int S, int RC, int RP>
+// CPT > 0: cin = 8 CPT at compile time (the staging's index divisions, the K loop's tap / chunk arithmetic and
+// its trip count become constants: the loop unrolls, every B read is base + a constant); 0: runtime cin.
+template <int S, int RC, int RP, int CPT = 0>
 __global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
   constexpr int TW = 16, TH = 4 * RP;
   constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
   extern __shared__ __attribute__((aligned(16))) h8 stile[];  // [RI][CI][cpt]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
-  const int cpt = a.cpt;
+  const int cpt = CPT ? CPT : a.cpt;
+  const int nsteps = CPT ? (9 * CPT + 3) / 4 : a.nsteps;
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   int t, cog;
   tile_block(a.gy, t, cog);
@@ -1308,16 +1311,17 @@ __global__ __launch_bounds__(256) void conv3x3_tile_small_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[r][p] = f4{0.f, 0.f, 0.f, 0.f};
   const h8 zero = h8{0, 0, 0, 0, 0, 0, 0, 0};
-  for (int st = 0; st < a.nsteps; ++st) {
+#pragma unroll
+  for (int st = 0; st < nsteps; ++st) {
     h8 af[RC];
 #pragma unroll
     for (int r = 0; r < RC; ++r) af[r] = an[r];
-    if (st + 1 < a.nsteps) {
+    if (st + 1 < nsteps) {
 #pragma unroll
       for (int r = 0; r < RC; ++r) an[r] = wfrag[r][(st + 1) * 64];
     }
     const unsigned c = unsigned(st * 4 + grp);
-    const int tap = cpt == 1 ? int(c) : int(__umulhi(c, a.cmagic));
+    const int tap = CPT ? int(c) / CPT : cpt == 1 ? int(c) : int(__umulhi(c, a.cmagic));
     const int ch = int(c) - tap * cpt;
     const bool tin = tap < 9;
     const int ky = (tap * 11) >> 5, kx = tap - ky * 3;  // tap / 3 for tap < 9
@@ -2349,12 +2353,23 @@ static void launch_tile3_s(const ConvArgs& a, int rc, int rp, int cw, int kp, bo
 
 template <int S, int RC>
 static void launch_small3_rc(const ConvArgs& a, int rp, dim3 grid, size_t lds, hipStream_t s) {
+  // compile-time cin for 8 and 16 channels (the n / s scales' small-cin 3x3s), runtime otherwise
+#define SMALL3(RPV)                                                                                     \
+  do {                                                                                                  \
+    if (a.cpt == 1)                                                                                     \
+      FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, RPV, 1>), grid, dim3(256), lds, s, a);               \
+    else if (a.cpt == 2)                                                                                \
+      FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, RPV, 2>), grid, dim3(256), lds, s, a);               \
+    else                                                                                                \
+      FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, RPV, 0>), grid, dim3(256), lds, s, a);               \
+  } while (0)
   if (rp == 1)
-    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 1>), grid, dim3(256), lds, s, a);
+    SMALL3(1);
   else if (rp == 2)
-    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 2>), grid, dim3(256), lds, s, a);
+    SMALL3(2);
   else
-    FCE_LAUNCH((conv3x3_tile_small_kernel<S, RC, 4>), grid, dim3(256), lds, s, a);
+    SMALL3(4);
+#undef SMALL3
 }
 
 template <int S>

@@ -32,7 +32,18 @@ static constexpr int RADIX_CAP = 8192;   // LDS radix sort capacity (16 waves x 
 static constexpr int REMOVED_CAP = 32768;
 static constexpr int KEPT_CAP = 1024;    // kept boxes held in LDS by the tiled path
 static constexpr int TILE = 64;
-static constexpr int WIN = 256;  // frontier extension step
+static constexpr int WIN = 256;  // frontier extension step (the multi-workgroup path)
+// the one-workgroup kernel's frontier step: candidates entering the window are tested against every box kept so
+// far, and those past the greedy's stop point are tested for nothing, so a short step wastes fewer tests at the
+// price of more extension rounds (FCE_NMS_WIN overrides, a multiple of 64)
+static int nms_win() {
+  static const int w = [] {
+    const char* e = getenv("FCE_NMS_WIN");
+    const int v = e ? atoi(e) : 256;
+    return v >= 64 && v % 64 == 0 ? v : 256;
+  }();
+  return w;
+}
 // small-set fast path: <= HEAD_CAP candidates sorted in LDS (1024 or 2048 slots instead of 8192).  Pool
 // layout of that sort:
 //   sort | keysA 8K | keysB 8K | valsA 4K | valsB 4K | wcnt (histogram) 16K |
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
                                                           float iou_thres, int max_det, int max_nms, float max_wh,
                                                           char* ws, size_t ws_per_image, float* dets, int64_t* keep,
                                                           int32_t* counts, int stop, int multi, int cap,
-                                                          NmsClassMask cm) {
+                                                          NmsClassMask cm, int win) {
   __shared__ __attribute__((aligned(16))) char pool[POOL];
   __shared__ int wsum[NWAVES];
   __shared__ int tile_idx[TILE];
@@ -651,7 +662,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
         tick(0);
         if (!s_need) break;
         // candidates entering the window: tested once against every box kept so far
-        const int Fn = min(Mg, F + WIN);
+        const int Fn = min(Mg, F + win);
         for (int j = F + threadIdx.x; j < Fn; j += NMS_THREADS) lremoved[j] = 0;
         __syncthreads();
         test_range(F, Fn, 0, s_kept);
@@ -1168,7 +1179,7 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
     FCE_LAUNCH(nms_best_class_kernel, dim3((A + 255) / 256, n), dim3(256), 0, s, pred, nc, A, max_nms,
                        static_cast<char*>(ws), per);
   FCE_LAUNCH(nms_kernel, dim3(n), dim3(NMS_THREADS), 0, s, pred, best, nc, A, conf, iou, max_det, max_nms, max_wh,
-                     static_cast<char*>(ws), per, dets, keep, counts, stop, multi, cap, cm);
+                     static_cast<char*>(ws), per, dets, keep, counts, stop, multi, cap, cm, nms_win());
   return launch_status("nms_kernel");
 }
 
