@@ -82,6 +82,28 @@ __device__ __forceinline__ float bias_or0(const float* b, int co, int n) {
   const float v = b[co < n ? co : n - 1];
   return co < n ? v : 0.f;
 }
+// fmaf((float)h, w, acc) for the low / high fp16 half h of a packed pair as ONE v_fma_mix_f32: the f16 -> f32
+// conversion is exact, so the result is bitwise the fmaf of the converted value (hipcc mixes this form with a
+// separate conversion + v_fma_f32 for the high halves, two VALU ops)
+__device__ __forceinline__ float fma_mix_lo(uint32_t hp, float w, float acc) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(w), "v"(acc));
+  return r;
+}
+__device__ __forceinline__ float fma_mix_hi(uint32_t hp, float w, float acc) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(w), "v"(acc));
+  return r;
+}
+// acc[j] = fmaf((float)v[j], w[j], acc[j]) for the 8 halves of v, as 8 v_fma_mix_f32
+__device__ __forceinline__ void fma8_mix(const h8& v, const float* w, float* acc) {
+  const u4 pk = __builtin_bit_cast(u4, v);
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    acc[2 * jj] = fma_mix_lo(pk[jj], w[2 * jj], acc[2 * jj]);
+    acc[2 * jj + 1] = fma_mix_hi(pk[jj], w[2 * jj + 1], acc[2 * jj + 1]);
+  }
+}
 // An fp32 value pinned in a register.  Without it hipcc fuses a multiply or add with the fp16
 // conversion that follows (v_fma_mix*: one rounding instead of two) in some kernels and not in
 // others, and conv variants that must be bitwise identical differ in the last fp16 bit.

@@ -1424,8 +1424,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwArgs a) {
     for (int p = 0; p < PX; ++p)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[p][j] = __builtin_fmaf((float)v[p * S + kx][j], wk[ky * 3 + kx][j], acc[p][j]);
+        fma8_mix(v[p * S + kx], wk[ky * 3 + kx], acc[p]);
   }
 #pragma unroll
   for (int p = 0; p < PX; ++p) {
@@ -1486,8 +1485,7 @@ __global__ __launch_bounds__(256) void dwconv_rows_kernel(DwArgs a, int CS) {
         if (ix < 0 || ix >= a.W) continue;
         const h8 v = rows[ky * RW + ix * (CS >> 3) + g];
         const float* wt = wl + (ky * 3 + kx) * CS + 8 * g;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fmaf((float)v[j], wt[j], acc[j]);
+        fma8_mix(v, wt, acc);
       }
     }
     h8 o;
@@ -1543,8 +1541,7 @@ __global__ __launch_bounds__(256) void dwconv_lanes_kernel(DwArgs a) {
         const int ix = ox * S - 1 + kx;
         if (ix < 0 || ix >= a.W) continue;
         const h8 v = *reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.W + ix) * a.xcs);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fmaf((float)v[j], wk[ky * 3 + kx][j], acc[j]);
+        fma8_mix(v, wk[ky * 3 + kx], acc);
       }
     }
     h8 o;
@@ -1614,9 +1611,14 @@ __global__ __launch_bounds__(256) void dwconv_cols_kernel(DwArgs a) {
       // an out-of-image tap loaded the zero line: fmaf(0, w, acc) == acc (the skipped tap of the other variants;
       // a select per FMA here was a third of the kernel's VALU work)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
+      for (int kx = 0; kx < 3; ++kx) {
+        const u4 pk = __builtin_bit_cast(u4, v[kx]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[p][j] = __builtin_fmaf((float)v[kx][j], wk[ky * 3 + kx][j], acc[p][j]);
+        for (int jj = 0; jj < 4; ++jj) {
+          acc[p][2 * jj] = fma_mix_lo(pk[jj], wk[ky * 3 + kx][2 * jj], acc[p][2 * jj]);
+          acc[p][2 * jj + 1] = fma_mix_hi(pk[jj], wk[ky * 3 + kx][2 * jj + 1], acc[p][2 * jj + 1]);
+        }
+      }
     }
   }
 #pragma unroll
