@@ -70,6 +70,8 @@ size_t coord_ws_bytes(const fce_coord_desc& d, int n, int h, int w) {
 }
 
 // ---------------------------------------------------------------------------- 1. pooling
+// sums of fp16 values as v_fma_mix_f32 (acc + h * 1: one op, bitwise the add of the converted half)
+static __device__ __constant__ float kOnes8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
 __device__ __forceinline__ void pool_rows(const _Float16* x, int xcs, int H, int W, int C, float* xh, int y, int n) {
   __shared__ float red[256 * 8];
   const int CG = C / 8;
@@ -80,8 +82,7 @@ __device__ __forceinline__ void pool_rows(const _Float16* x, int xcs, int H, int
   if (xt < XT) {
     for (int xx = xt; xx < W; xx += XT) {
       const h8 v = *reinterpret_cast<const h8*>(x + nhwc_off(n, y, xx, H, W, xcs) + cg * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+      fma8_mix(v, kOnes8, acc);
     }
   }
 #pragma unroll
@@ -127,13 +128,11 @@ __device__ __forceinline__ void pool_cols(const _Float16* x, int xcs, int H, int
       for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const h8*>(p + (y + k) * rs);
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += (float)v[k][j];
+        fma8_mix(v[k], kOnes8, acc);
     }
     for (; y < y1; ++y) {
       const h8 v0 = *reinterpret_cast<const h8*>(p + y * rs);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += (float)v0[j];
+      fma8_mix(v0, kOnes8, acc);
     }
   }
 #pragma unroll
@@ -210,13 +209,10 @@ __global__ __launch_bounds__(256) void pool_band_kernel(const _Float16* x, int x
     }
     float r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < KW; ++k)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (float)v[k][j];
-        col[k][j] += f;
-        r[j] += f;
-      }
+    for (int k = 0; k < KW; ++k) {
+      fma8_mix(v[k], kOnes8, col[k]);
+      fma8_mix(v[k], kOnes8, r);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       r[j] += __shfl_xor(r[j], 8);
@@ -917,11 +913,13 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
       wv[4] = gb[k][1][0]; wv[5] = gb[k][1][1]; wv[6] = gb[k][1][2]; wv[7] = gb[k][1][3];
     }
     h8 o;
+    const u4 pk = __builtin_bit_cast(u4, v[k]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float r;
-      if (MODE == GATE_BICOORD)
-        r = (float)v[k][j] * sigmoidf_(gv[j] + wv[j]);  // v_exp + v_rcp (the gate is VALU-bound)
+      if (MODE == GATE_BICOORD)  // v_exp + v_rcp; x * g as v_fma_mix_f32(x, g, -0): bitwise the product, no conversion
+        r = (j & 1) ? fma_mix_hi(pk[j >> 1], sigmoidf_(gv[j] + wv[j]), -0.0f)
+                    : fma_mix_lo(pk[j >> 1], sigmoidf_(gv[j] + wv[j]), -0.0f);
       else if (MODE == GATE_COORD)
         r = (float)v[k][j] * gv[j] * wv[j];
       else
