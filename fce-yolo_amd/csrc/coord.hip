@@ -913,13 +913,11 @@ __global__ __launch_bounds__(256) void gate_apply_kernel(const _Float16* x, int 
       wv[4] = gb[k][1][0]; wv[5] = gb[k][1][1]; wv[6] = gb[k][1][2]; wv[7] = gb[k][1][3];
     }
     h8 o;
-    const u4 pk = __builtin_bit_cast(u4, v[k]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float r;
-      if (MODE == GATE_BICOORD)  // v_exp + v_rcp; x * g as v_fma_mix_f32(x, g, -0): bitwise the product, no conversion
-        r = (j & 1) ? fma_mix_hi(pk[j >> 1], sigmoidf_(gv[j] + wv[j]), -0.0f)
-                    : fma_mix_lo(pk[j >> 1], sigmoidf_(gv[j] + wv[j]), -0.0f);
+      if (MODE == GATE_BICOORD)
+        r = (float)v[k][j] * sigmoidf_(gv[j] + wv[j]);  // v_exp + v_rcp (the gate is VALU-bound)
       else if (MODE == GATE_COORD)
         r = (float)v[k][j] * gv[j] * wv[j];
       else
