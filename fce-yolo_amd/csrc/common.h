@@ -84,7 +84,9 @@ __device__ __forceinline__ float bias_or0(const float* b, int co, int n) {
 }
 // fmaf((float)h, w, acc) for the low / high fp16 half h of a packed pair as ONE v_fma_mix_f32: the f16 -> f32
 // conversion is exact, so the result is bitwise the fmaf of the converted value (hipcc mixes this form with a
-// separate conversion + v_fma_f32 for the high halves, two VALU ops)
+// separate conversion + v_fma_f32 for the high halves, two VALU ops).  Only for operands that come from loads or
+// ordinary VALU ops: hipcc's hazard recognizer does not see inside inline asm, and the BiCoord gate fed a v_rcp_f32
+// result straight into one of these and read wrong values (bicoord parity failed; reverted there)
 __device__ __forceinline__ float fma_mix_lo(uint32_t hp, float w, float acc) {
   float r;
   asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(w), "v"(acc));
