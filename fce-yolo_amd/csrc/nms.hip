@@ -286,13 +286,20 @@ __device__ __forceinline__ float iou_ref(float4 bi, float ai, float4 bj, float a
   return inter / ((ai + aj) - inter);
 }
 
-// iou_ref(...) > thr for positive areas: a zero intersection gives IoU 0 (thr >= 0), skip the division
+// iou_ref(...) > thr for positive areas: a zero intersection gives IoU 0 (thr >= 0), skip the division.  The IEEE
+// division (~10 VALU ops) runs only when inter is within 2^-20 of thr * union: p = RN(thr * union) is within 2^-24 of
+// the real product, so inter > p (1 + 2^-20) puts the real quotient above thr by far more than the half ulp RN(q)
+// could lose (RN(q) > thr, as the reference computes it), and inter < p (1 - 2^-20) puts it below thr.  Exact.
 __device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float aj, float thr) {
   const float ww = fmaxf(fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x), 0.0f);
   const float hh = fmaxf(fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y), 0.0f);
   const float inter = ww * hh;
   if (inter == 0.0f) return false;
-  return inter / ((ai + aj) - inter) > thr;
+  const float uni = (ai + aj) - inter;
+  const float p = thr * uni;
+  if (inter > p * 1.00000095367431640625f) return true;    // 1 + 2^-20
+  if (inter < p * 0.99999904632568359375f) return false;   // 1 - 2^-20
+  return inter / uni > thr;
 }
 
 // best class per anchor (first maximum, like torch.max): one thread per (image, anchor), all CUs
