@@ -1178,7 +1178,9 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs a) {
 // range [x chunk, (x + 1) chunk) and its slot-th blocks take tiles x chunk + slot + k nslot, so the tiles
 // whose halos overlap are in flight on one XCD's L2 at the same time.
 // K order (chunk, tap) is the implicit-GEMM kernel's: bitwise identical.
-template <int S, int RP, int NCH>
+// PD = 2 (round 4): two register sets of staged input, the loop unrolled by two so each set's loads are issued two
+// tiles ahead of their LDS store (two compute phases to land instead of one).
+template <int S, int RP, int NCH, int PD = 1>
 __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot) {
   constexpr int TW = 16, TH = RP;
   constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
@@ -1222,17 +1224,16 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
                   : reinterpret_cast<const h8*>(g_zero_line));
     }
   };
-  h8 v[NL];
-  int sl[NL];
-  stage_load(t, v, sl);
+  h8 v[NL], v2[NL];
+  int sl[NL], sl2[NL];
   const int step = nslot;
-  for (int cur = 0; t < tend; cur ^= 1) {
+  // one tile: vv holds its staged input; vv is then reloaded with the tile PD steps on
+  auto iter = [&](h8 (&vv)[NL], int (&ss)[NL], int cur) {
 #pragma unroll
-    for (int i = 0; i < NL; ++i) tile[cur * BUF + sl[i]] = v[i];
+    for (int i = 0; i < NL; ++i) tile[cur * BUF + ss[i]] = vv[i];
     __syncthreads();
-    const int tn = t + step;
     const int tx = t % tiles_x, r0 = t / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
-    if (tn < tend) stage_load(tn, v, sl);
+    if (t + PD * step < tend) stage_load(t + PD * step, vv, ss);
     f4 acc[1][RP];
 #pragma unroll
     for (int p = 0; p < RP; ++p) acc[0][p] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1249,7 +1250,20 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
         }
       }
     tile3_store<1, RP>(a, acc, n, ty * TH, tx * TW, cot0, col, grp);
-    t = tn;
+    t += step;
+  };
+  stage_load(t, v, sl);
+  if (PD == 1) {
+    for (int cur = 0; t < tend; cur ^= 1) iter(v, sl, cur);
+  } else {
+    if (t + step < tend) stage_load(t + step, v2, sl2);
+    for (int cur = 0; t < tend;) {
+      iter(v, sl, cur);
+      cur ^= 1;
+      if (t >= tend) break;
+      iter(v2, sl2, cur);
+      cur ^= 1;
+    }
   }
 }
 
@@ -2260,7 +2274,8 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     }
   if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.up == 0 && !det_box && !no_ring())  // persistent: 0x600 | rp << 4
     for (int rp : {1, 2, 4})
-      if (n < cap) out[n++] = 0x600 | (rp << 4);
+      for (int pd : {1, 2})
+        if (n < cap) out[n++] = 0x600 | (rp << 4) | (pd - 1);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel: 0x100 | rc | rp << 4 | cw, kp bits
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
@@ -2417,25 +2432,34 @@ static int launch_tile3(const ConvArgs& a, int rc, int rp, int cw, int kp, bool 
   return launch_status("conv3x3_tile_kernel");
 }
 
-template <int S, int RP, int NCH>
+template <int S, int RP, int NCH, int PD>
 static void launch_ring3_k(const ConvArgs& a, dim3, int ntiles, hipStream_t s) {
-  static const int occ = blocks_per_cu(conv3x3_ring_kernel<S, RP, NCH>, 0);
+  static const int occ = blocks_per_cu(conv3x3_ring_kernel<S, RP, NCH, PD>, 0);
   const int nslot = ring_slots(ntiles, a.gy, occ);
-  FCE_LAUNCH((conv3x3_ring_kernel<S, RP, NCH>), dim3(unsigned(8 * a.gy * nslot)), dim3(256), 0, s, a, nslot);
+  FCE_LAUNCH((conv3x3_ring_kernel<S, RP, NCH, PD>), dim3(unsigned(8 * a.gy * nslot)), dim3(256), 0, s, a, nslot);
 }
 
 template <int S, int NCH>
-static void launch_ring3_s(const ConvArgs& a, int rp, dim3 grid, int nslot, hipStream_t s) {
-  if (rp == 1)
-    launch_ring3_k<S, 1, NCH>(a, grid, nslot, s);
-  else if (rp == 2)
-    launch_ring3_k<S, 2, NCH>(a, grid, nslot, s);
-  else
-    launch_ring3_k<S, 4, NCH>(a, grid, nslot, s);
+static void launch_ring3_s(const ConvArgs& a, int rp, int pd, dim3 grid, int nslot, hipStream_t s) {
+  if (pd == 2) {
+    if (rp == 1)
+      launch_ring3_k<S, 1, NCH, 2>(a, grid, nslot, s);
+    else if (rp == 2)
+      launch_ring3_k<S, 2, NCH, 2>(a, grid, nslot, s);
+    else
+      launch_ring3_k<S, 4, NCH, 2>(a, grid, nslot, s);
+  } else if (rp == 1) {
+    launch_ring3_k<S, 1, NCH, 1>(a, grid, nslot, s);
+  } else if (rp == 2) {
+    launch_ring3_k<S, 2, NCH, 1>(a, grid, nslot, s);
+  } else {
+    launch_ring3_k<S, 4, NCH, 1>(a, grid, nslot, s);
+  }
 }
 
 
-static int launch_ring3(const ConvArgs& a0, int rp, int stride, hipStream_t s) {
+// pd: tiles of staged input in flight ahead of the LDS store (1, or 2: two register sets)
+static int launch_ring3(const ConvArgs& a0, int rp, int pd, int stride, hipStream_t s) {
   FCE_CHECK((a0.cin == 32 || a0.cin == 64) && (rp == 1 || rp == 2 || rp == 4), "conv 3x3 ring: bad configuration");
   ConvArgs a = a0;
   const int nch = a.cin / 32;
@@ -2445,9 +2469,9 @@ static int launch_ring3(const ConvArgs& a0, int rp, int stride, hipStream_t s) {
   const int nslot = int(ntiles);  // the leaf launcher turns the tile count into slots (occupancy)
   const dim3 grid(1);
   if (stride == 1)
-    nch == 1 ? launch_ring3_s<1, 1>(a, rp, grid, nslot, s) : launch_ring3_s<1, 2>(a, rp, grid, nslot, s);
+    nch == 1 ? launch_ring3_s<1, 1>(a, rp, pd, grid, nslot, s) : launch_ring3_s<1, 2>(a, rp, pd, grid, nslot, s);
   else
-    nch == 1 ? launch_ring3_s<2, 1>(a, rp, grid, nslot, s) : launch_ring3_s<2, 2>(a, rp, grid, nslot, s);
+    nch == 1 ? launch_ring3_s<2, 1>(a, rp, pd, grid, nslot, s) : launch_ring3_s<2, 2>(a, rp, pd, grid, nslot, s);
   return launch_status("conv3x3_ring_kernel");
 }
 
@@ -2713,8 +2737,9 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   }
   if (kind == 6) {  // persistent 3x3 ring, A in registers
     rp = (tile >> 4) & 15;
-    FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && out_kind == OUT_F16 && d.up == 0, "conv: bad 3x3 ring hint");
-    return launch_ring3(a, rp, d.stride, s);
+    FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && out_kind == OUT_F16 && d.up == 0 && (tile & 14) == 0,
+              "conv: bad 3x3 ring hint");
+    return launch_ring3(a, rp, (tile & 1) ? 2 : 1, d.stride, s);  // 0x601: two tiles of input in flight
   }
   if (kind == 8) {  // big-tile LDS-DMA 3x3 kernel
     const int wm = (tile >> 4) & 15, ab = ((tile >> 12) & 1) + 2, nw = 4;
