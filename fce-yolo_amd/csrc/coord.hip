@@ -1057,13 +1057,16 @@ static int launch_core(const fce_coord_desc& d, const CoordWs& w, int N, int H, 
   a.heads = d.heads;
   a.oup = d.oup;
   a.scale = d.scale;
-  // query chunks: 2 N (image, branch) workgroups alone leave most CUs idle; up to 4 chunks of at least
+  // query chunks: 2 N (image, branch) workgroups alone leave most CUs idle; up to 2 chunks of at least
   // 8 queries.  The split depends on the map size only, never on N: the chunk size sets the attention's
   // key split, so a batch-dependent split would break batch invariance (test_batch_invariance_640).
   {
     const int L = H < W ? H : W;
     int qs = 1;
-    while (qs < 4 && L / (2 * qs) >= 8) qs *= 2;
+    // each chunk's workgroup stages and projects the whole axis again, so with several batches in flight fewer
+    // chunks are cheaper overall: n32 (4 lanes) 36.5k images/s with 4 chunks, 36.8-37.0k with 2, 37.0k with 1
+    // (profiles/r04ai_qsplit*, FCE_COORD_QSPLIT); 2 keeps part of the split for one-batch latency
+    while (qs < 2 && L / (2 * qs) >= 8) qs *= 2;
     const char* qe = getenv("FCE_COORD_QSPLIT");  // diagnostics: force the query split
     if (qe && atoi(qe) > 0) qs = atoi(qe);
     a.qsplit = qs;
