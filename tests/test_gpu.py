@@ -428,6 +428,57 @@ def test_nms_equal_top_score_group(case, device, nms_path):
             assert np.array_equal(dets[b].cpu().numpy(), od[b]), (b, max_det)
 
 
+def _iou_fp32(b1, b2):
+    """The reference's IoU (nms.py:276-291) in fp32 on xywh pairs (xywh2xyxy as ops.py:224-240), vectorised."""
+    f = np.float32
+    x1 = [b1[0] - b1[2] / f(2), b1[1] - b1[3] / f(2), b1[0] + b1[2] / f(2), b1[1] + b1[3] / f(2)]
+    x2 = [b2[0] - b2[2] / f(2), b2[1] - b2[3] / f(2), b2[0] + b2[2] / f(2), b2[1] + b2[3] / f(2)]
+    a1 = (x1[2] - x1[0]) * (x1[3] - x1[1])
+    a2 = (x2[2] - x2[0]) * (x2[3] - x2[1])
+    ww = np.maximum(np.minimum(x1[2], x2[2]) - np.maximum(x1[0], x2[0]), f(0))
+    hh = np.maximum(np.minimum(x1[3], x2[3]) - np.maximum(x1[1], x2[1]), f(0))
+    inter = ww * hh
+    return inter / ((a1 + a2) - inter)
+
+
+@pytest.mark.parametrize("thr", [0.7, 0.45])
+def test_nms_iou_at_the_threshold(thr, device, nms_path):
+    """Box pairs whose fp32 IoU lies within a few ulps of iou_thres, on both sides (2e5 random pairs per slot, the
+    closest kept; measured ~8 ulps at 0.7): the kernel
+    decides `IoU > thr` without the IEEE division unless inter is within 2^-20 of thr * union (nms.py:276-291
+    computes the quotient), so these pairs take the exact fallback.  Kept indices and rows bit-exact vs the oracle."""
+    rng = np.random.default_rng(int(thr * 100))
+    f = np.float32
+    slots, tries = 64, 200_000
+    A = 2 * slots
+    p = np.zeros((1, 5, A), f)
+    got = []
+    for s_ in range(slots):
+        cx, cy = f(30 + 90 * (s_ % 8)), f(30 + 90 * (s_ // 8))
+        w1, h1 = rng.uniform(20, 40, tries).astype(f), rng.uniform(20, 40, tries).astype(f)
+        w2, h2 = (w1 * rng.uniform(0.8, 1.2, tries)).astype(f), (h1 * rng.uniform(0.8, 1.2, tries)).astype(f)
+        dx, dy = rng.uniform(-8, 8, tries).astype(f), rng.uniform(-8, 8, tries).astype(f)
+        b1 = [np.full(tries, cx, f), np.full(tries, cy, f), w1, h1]
+        b2 = [cx + dx, cy + dy, w2, h2]
+        iou = _iou_fp32(b1, b2)
+        want = [-1, 0, 1][s_ % 3]  # just below, as close as possible, just above
+        d = (iou.astype(np.float64) - thr) * [1, 1, -1][s_ % 3]
+        d = np.where((d <= 0) if want != 0 else np.ones_like(d, bool), np.abs(d), np.inf)
+        k = int(np.argmin(d))
+        got.append(float(iou[k]))
+        for j, b in enumerate((b1, b2)):
+            p[0, :4, 2 * s_ + j] = [b[0][k], b[1][k], b[2][k], b[3][k]]
+        p[0, 4, 2 * s_] = f(0.9)
+        p[0, 4, 2 * s_ + 1] = f(0.8)
+    got = np.array(got)
+    assert np.abs(got - thr).max() < 1e-5 and (got > f(thr)).any() and (got <= f(thr)).any()
+    pt = torch.from_numpy(p).to(device)
+    dets, keep = non_max_suppression(pt, 0.25, thr, 300, return_idxs=True)
+    od, ok = nms_oracle.non_max_suppression(p, 0.25, thr)
+    assert np.array_equal(keep[0].cpu().numpy(), ok[0]) and np.array_equal(dets[0].cpu().numpy(), od[0])
+    assert len(ok[0]) == slots + int((got <= f(thr)).sum())  # every pair: the second box survives iff IoU <= thr
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_nms_clustered_suppression_chains(seed, device, nms_path):
     """Heavy, chained suppression: jittered boxes around a few centres, few classes, tied (quantised)
