@@ -57,6 +57,31 @@ def test_mfma_conv_exact_integer(device):
         assert torch.equal(y.double().cpu(), ref), (cin, cout, k)
 
 
+@pytest.mark.parametrize("cin,cout,H,W", [(3, 16, 64, 96), (3, 32, 40, 48), (1, 16, 34, 72), (2, 48, 30, 40),
+                                            (3, 64, 66, 64)])
+def test_stem_mfma_parity(cin, cout, H, W, device):
+    """The MFMA stem (first Conv, 3x3 s2 on the NCHW network input, k = ci * 9 + tap zero-padded to one 32-deep
+    K-step: the padded k slots re-read a real tap, their weights are zero) against a plain torch fp32 Conv + BN +
+    SiLU on the same fp16 input, for 1-3 input channels, 16-64 outputs, odd / ragged maps."""
+    torch.manual_seed(cin * 100 + cout)
+    conv = M.Conv(cin, cout, 3, 2)
+    with torch.no_grad():
+        conv.conv.weight.normal_(0, 0.3)
+        conv.bn.weight.uniform_(0.5, 1.5)
+        conv.bn.bias.normal_(0, 0.2)
+        conv.bn.running_mean.normal_(0, 0.1)
+        conv.bn.running_var.uniform_(0.5, 1.5)
+    conv.eval()
+    x = torch.rand(2, cin, H, W).half()
+    with torch.no_grad():
+        ref = torch.nn.functional.silu(conv.bn(conv.conv(x.float())))
+        y = conv.to(device)(x.to(device))
+    assert tuple(y.shape) == tuple(ref.shape)
+    err = _rel(y.float(), ref)
+    print(f"OPERR stem {cin}->{cout} {err:.3e}")
+    assert err <= OP_TOL, err
+
+
 @pytest.mark.parametrize("name", list(cases.OPS))
 def test_op_parity(name, ops_fx, device):
     fx = ops_fx.group(name)
