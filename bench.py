@@ -55,9 +55,9 @@ def launch_command(argv, env):
 
 def default_lanes(model: str, env, gpus: int = 1) -> int:
     """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n and s scales on one GPU
-    (n32 29.3-29.6k vs 28.7-28.8k images/s with 3, s32 16.0-16.1k vs 15.8k, profiles/r03w_*, r03ak_*) and 3
-    otherwise: the m / l scales, whose four arenas overflow the MALL (l32 4 954 vs 4 573, m16-h8 1 625 vs 1 529
-    images/s with 4, profiles/r03y_*), and every run with a
+    (n32 29.3-29.6k vs 28.7-28.8k images/s with 3, s32 16.0-16.1k vs 15.8k, profiles/r03w_*, r03ak_*) and, since
+    round 4's faster kernels, the l scale (l32 5.64-5.65k vs 5.57-5.58k, profiles/r04aq_*); 3 otherwise: the m scale,
+    whose four arenas overflow the MALL (m16-h8 1.83k vs 1.76k images/s with 4, profiles/r04aq_*), and every run with a
     process group, where RCCL's streams share the hardware queues (one-rank RCCL path 27.8k with 3 lanes x 4 queues,
     24.8-25.3k with 4 x 8, profiles/r03ad_*)."""
     if env.get("FCE_LANES"):
@@ -66,7 +66,7 @@ def default_lanes(model: str, env, gpus: int = 1) -> int:
         return 3
     stem = Path(model).stem
     scale = stem[6:7] if stem.startswith("yolo11") else ""
-    return 4 if scale in ("n", "s") else 3
+    return 4 if scale in ("n", "s", "l") else 3
 
 
 def hw_queues_env(argv, env):
