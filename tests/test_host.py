@@ -247,10 +247,11 @@ def test_bench_gpus_n_launches_ranks_before_torch():
     assert m.hw_queues_env([], {}) == "8" and m.hw_queues_env([], {"GPU_MAX_HW_QUEUES": "4"}) == "8"
     assert m.hw_queues_env([], {"GPU_MAX_HW_QUEUES": "16"}) is None
     assert m.hw_queues_env(["--lanes", "3"], {}) is None and m.hw_queues_env([], {"FCE_LANES": "2"}) is None
-    # lanes default by scale: 4 for n, 3 for the wider models (their activation arenas overflow the MALL)
+    # lanes default by scale: 4 for n / s / l, 3 for m at 1280 (its activation arenas overflow the MALL)
     assert m.default_lanes("yolo11n-fce.yaml", {}) == 4 and m.default_lanes("yolo11l-fce.yaml", {}) == 4
     assert m.default_lanes("yolo11m-fce-h8.yaml", {}) == 3 and m.default_lanes("yolo11s-bifpn.yaml", {}) == 4
-    assert m.hw_queues_env(["--model", "yolo11l-fce.yaml"], {}) is None
+    assert m.hw_queues_env(["--model", "yolo11l-fce.yaml"], {}) == "8"
+    assert m.hw_queues_env(["--model", "yolo11m-fce-h8.yaml"], {}) is None
     # with a process group (N > 1, a rank, or the one-rank RCCL rehearsal): 3 lanes, HIP's queues untouched
     assert m.default_lanes("yolo11n-fce.yaml", {}, 8) == 3 and m.default_lanes("yolo11n-fce.yaml", {"WORLD_SIZE": "8"}) == 3
     assert m.hw_queues_env(["--gpus", "8"], {}) is None and m.hw_queues_env([], {"WORLD_SIZE": "2"}) is None
