@@ -486,11 +486,142 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
   // ---- 2h. small candidate sets (<= HEAD_CAP, the usual case for a trained model) are sorted in 1024 or
   // 2048 LDS slots instead of RADIX_CAP (FCE_NMS_STOP=3, diagnostics: always the full sort)
   int hn = 0;
-  bool head = false;
-  if (tiled && stop != 3) {
+  bool head = false, prefix_only = false;
+  if (tiled && stop != 3 && stop != 10) {
     hn = ncand;
     head = hn <= HEAD_CAP && hn > 0;
-    if (head) {
+    if (!head && hn <= RADIX_CAP) {
+      // ---- 2s. more than HEAD_CAP candidates: only the first HEAD_CAP entries of the sorted order (score desc,
+      // position asc) are sorted.  A radix select (four 8-bit digit passes over the score bits held in registers,
+      // wave-aggregated LDS atomics, three rotating histograms so each pass has one barrier, every wave finding
+      // the digit itself) gives the HEAD_CAP-th largest score T and how many of the candidates scoring exactly T
+      // the prefix takes (`need`: the first ones in position order, as the sort's tie order has it).  One ballot
+      // scan over (chunk, wave) counts of the candidates above T and at T places the prefix in position order
+      // and the 2048-slot sort orders it.  The greedy over the prefix is the full greedy's when max_det is reached
+      // inside it; otherwise the full sort runs (attempt 1 below).
+      constexpr int KPT = RADIX_CAP / NMS_THREADS;
+      int* hist = reinterpret_cast<int*>(pool + H_OFF_WC);  // 3 x 256 bins, rotating over the passes
+      int* gsel = hist + 3 * 256;                           // [KPT * NWAVES] above T, then [KPT * NWAVES] at T
+      uint32_t key[KPT];
+#pragma unroll
+      for (int k = 0; k < KPT; ++k) {
+        const int idx = k * NMS_THREADS + int(threadIdx.x);
+        key[k] = idx < hn ? __float_as_uint(w.cscore[idx]) : 0u;  // scores > conf >= 0: valid keys > 0
+      }
+      if (threadIdx.x < 512) hist[threadIdx.x] = 0;
+      __syncthreads();
+      uint32_t pre = 0, pmask = 0;
+      int need = HEAD_CAP;
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        int* h = hist + 256 * (pass % 3);
+        // the histogram of pass + 1 was last read after the barrier of pass - 2: every wave is past that read
+        if (pass > 0 && threadIdx.x < 256) hist[256 * ((pass + 1) % 3) + threadIdx.x] = 0;
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+          // the lanes sharing the first active lane's digit add once (saturated scores put most keys in one
+          // bin for the top digits; same-address LDS atomics would serialise)
+          const bool in = k * NMS_THREADS + int(threadIdx.x) < hn && (key[k] & pmask) == pre;
+          const int d = int(key[k] >> shift) & 255;
+          const uint64_t act = __ballot(in);
+          if (act) {
+            const int first = __builtin_ctzll(act);
+            const int d0 = __shfl(d, first);
+            const uint64_t same = __ballot(in && d == d0);
+            if (lane == first) atomicAdd(&h[d0], __popcll(same));
+            if (in && d != d0) atomicAdd(&h[d], 1);
+          }
+        }
+        __syncthreads();
+        // every wave: lane l holds digits 4l .. 4l+3; the digit whose bin holds the need-th largest key
+        int hv[4], s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          hv[i] = h[4 * lane + i];
+          s += hv[i];
+        }
+        int inc = s;  // suffix sum over lanes >= lane
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_down(inc, o);
+          if (lane + o < 64) inc += y;
+        }
+        int above = inc - s, myd = 0, myab = 0;
+        bool found = false;
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+          if (above < need && need <= above + hv[i]) {
+            found = true;
+            myd = 4 * lane + i;
+            myab = above;
+          }
+          above += hv[i];
+        }
+        const int src = __builtin_ctzll(__ballot(found));
+        pre |= uint32_t(__shfl(myd, src)) << shift;
+        pmask |= 255u << shift;
+        need -= __shfl(myab, src);
+      }
+      // pre = T; the prefix = every candidate above T and the first `need` at T in position order
+#pragma unroll
+      for (int k = 0; k < KPT; ++k) {
+        const bool valid = k * NMS_THREADS + int(threadIdx.x) < hn;
+        const uint64_t ma = __ballot(valid && key[k] > pre), mt = __ballot(valid && key[k] == pre);
+        if (lane == 0) {
+          gsel[k * NWAVES + wv] = __popcll(ma);
+          gsel[KPT * NWAVES + k * NWAVES + wv] = __popcll(mt);
+        }
+      }
+      __syncthreads();
+      if (wv == 0) {  // two exclusive scans in (chunk, wave) = position order
+        constexpr int PER = (KPT * NWAVES + 63) / 64;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          int* g = gsel + half * KPT * NWAVES;
+          int v[PER], sum = 0;
+#pragma unroll
+          for (int k = 0; k < PER; ++k) {
+            v[k] = g[lane * PER + k];
+            sum += v[k];
+          }
+          int inc = sum;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+          }
+          int ex = inc - sum;
+#pragma unroll
+          for (int k = 0; k < PER; ++k) {
+            g[lane * PER + k] = ex;
+            ex += v[k];
+          }
+        }
+      }
+      __syncthreads();
+      uint32_t* kA = reinterpret_cast<uint32_t*>(pool + H_OFF_KA);
+      uint16_t* vA = reinterpret_cast<uint16_t*>(pool + H_OFF_VA);
+#pragma unroll
+      for (int k = 0; k < KPT; ++k) {
+        const int idx = k * NMS_THREADS + int(threadIdx.x);
+        const bool valid = idx < hn, ab = valid && key[k] > pre, at = valid && key[k] == pre;
+        const uint64_t ma = __ballot(ab), mt = __ballot(at);
+        const int nab = gsel[k * NWAVES + wv] + __popcll(ma & lt);               // above T before me
+        const int nat = gsel[KPT * NWAVES + k * NWAVES + wv] + __popcll(mt & lt);  // at T before me
+        if (ab || (at && nat < need)) {
+          const int pos = nab + min(nat, need);
+          kA[pos] = ~key[k];
+          vA[pos] = uint16_t(idx);
+        }
+      }
+      __syncthreads();
+      radix_sort_lds<2>(kA, reinterpret_cast<uint32_t*>(pool + H_OFF_KB), vA,
+                        reinterpret_cast<uint16_t*>(pool + H_OFF_VB), reinterpret_cast<int*>(pool + H_OFF_WC), wsum);
+      __syncthreads();
+      hn = HEAD_CAP;
+      head = prefix_only = true;
+    } else if (head) {
       uint32_t* kA = reinterpret_cast<uint32_t*>(pool + H_OFF_KA);
       uint16_t* vA = reinterpret_cast<uint16_t*>(pool + H_OFF_VA);
       const int cap = hn <= 1024 ? 1024 : 2048;
@@ -510,7 +641,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
   }
   if (stop == 2) return;
 
-  for (int attempt = head ? 0 : 1; attempt < 2; ++attempt) {  // one pass: the small or the full sort
+  for (int attempt = head ? 0 : 1; attempt < 2; ++attempt) {  // the small (or prefix) sort, else the full sort
     const bool H = attempt == 0;
     int Mg = M;  // sorted positions this attempt covers
     bool lds_sorted = true;
@@ -543,6 +674,8 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
           w.spos[i] = int(0xFFFFFFFFu - uint32_t(w.keys[i] & 0xFFFFFFFFull));
         __syncthreads();
       }
+      __syncthreads();
+      if (stop == 10) return;  // phase timing (diagnostics only): the full sort's cost
     }
     auto sp = [&](int i) -> int { return lds_sorted ? int(spos16[i]) : w.spos[i]; };
     // greedy state over the dead sort keys (the sorted positions, spos16, stay live in either layout)
@@ -743,6 +876,9 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
       tick(3);
     }
     __syncthreads();
+    // the selected prefix ran out before max_det: its decisions are the full greedy's, but the greedy goes on
+    // past it, so start again over the full sort
+    if (H && prefix_only && !reached && Mg < M) continue;
     tick(7);
     for (int slot = threadIdx.x; slot < s_kept; slot += NMS_THREADS) emit_det(kidx[slot], slot);
     __syncthreads();

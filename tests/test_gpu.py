@@ -527,6 +527,31 @@ def test_nms_clustered_suppression_chains(seed, device, nms_path):
             assert np.array_equal(dets[b].cpu().numpy(), od[b]), (iou, max_det, b)
 
 
+@pytest.mark.parametrize("max_nms,max_det", [(1500, 300), (3000, 300), (30000, 3000), (30000, 40)])
+def test_nms_sorted_prefix_select(max_nms, max_det, device, nms_path):
+    """2049..8192 candidates: the first 2048 of the order (score desc, position asc) selected by a radix select
+    over score bits << 13 | (8191 - position) and sorted alone; the full sort when the greedy runs out of the
+    prefix (max_det 3000; heavy suppression with max_det 40) or max_nms truncates inside it (1500).  Most
+    scores tied, the tied group straddling the 2048-th position.  Bit-exact vs the oracle."""
+    rng = np.random.default_rng(21)
+    B, A, nc = 2, 7000, 5
+    p = np.zeros((B, 4 + nc, A), np.float32)
+    tight = max_det == 40  # one class, 24 piles: the 40th kept box at sorted depth 2324 / 1463 (past / inside 2048)
+    for b in range(B):
+        c = rng.random((24 if tight else 60, 2)) * 600 + 20
+        k = rng.integers(0, len(c), A)
+        p[b, 0:2] = (c[k] + rng.normal(0, 1.5 if tight else 12, (A, 2))).T
+        p[b, 2:4] = (rng.random((A, 2)) * (2 if tight else 10) + 40).T
+        sc = np.where(rng.random(A) < 0.6, np.float32(0.875), 0.3 + 0.69 * rng.random(A)).astype(np.float32)
+        p[b, 4 + rng.integers(0, 1 if tight else nc, A), np.arange(A)] = sc
+    pt = torch.from_numpy(p).to(device)
+    dets, keep = non_max_suppression(pt, 0.25, 0.7, max_det, max_nms=max_nms, return_idxs=True)
+    od, ok = nms_oracle.non_max_suppression(p, 0.25, 0.7, max_det=max_det, max_nms=max_nms)
+    for b in range(B):
+        assert np.array_equal(keep[b].cpu().numpy(), ok[b]), b
+        assert np.array_equal(dets[b].cpu().numpy(), od[b]), b
+
+
 @pytest.mark.parametrize("case", ["bench_like", "unbanded", "one_class_heavy"])
 def test_nms_top_selection_and_class_buckets(case, device, nms_path):
     """The large-candidate-set paths against the oracle: top-1024 selection (MSB radix select on tied
