@@ -290,16 +290,31 @@ __device__ __forceinline__ float iou_ref(float4 bi, float ai, float4 bj, float a
 // division (~10 VALU ops) runs only when inter is within 2^-20 of thr * union: p = RN(thr * union) is within 2^-24 of
 // the real product, so inter > p (1 + 2^-20) puts the real quotient above thr by far more than the half ulp RN(q)
 // could lose (RN(q) > thr, as the reference computes it), and inter < p (1 - 2^-20) puts it below thr.  Exact.
+// min / max of finite floats without the NaN-quieting canonicalisation fminf / fmaxf get in IEEE mode (two
+// extra v_max per operand, re-done every iteration even for loop-invariant boxes): the same value for every
+// finite input, and every box here is finite (degenerate boxes take the literal path)
+__device__ __forceinline__ float vmin_(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax_(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ bool suppresses(float4 bi, float ai, float4 bj, float aj, float thr) {
-  const float ww = fmaxf(fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x), 0.0f);
-  const float hh = fmaxf(fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y), 0.0f);
+  const float ww = vmax_(vmin_(bi.z, bj.z) - vmax_(bi.x, bj.x), 0.0f);
+  const float hh = vmax_(vmin_(bi.w, bj.w) - vmax_(bi.y, bj.y), 0.0f);
   const float inter = ww * hh;
-  if (inter == 0.0f) return false;
   const float uni = (ai + aj) - inter;
   const float p = thr * uni;
-  if (inter > p * 1.00000095367431640625f) return true;    // 1 + 2^-20
-  if (inter < p * 0.99999904632568359375f) return false;   // 1 - 2^-20
-  return inter / uni > thr;
+  const bool hi = inter > p * 1.00000095367431640625f;  // 1 + 2^-20
+  const bool lo = inter < p * 0.99999904632568359375f;  // 1 - 2^-20 (inter == 0 < p: lo, when thr > 0)
+  bool r = hi;
+  if (!(hi || lo)) r = inter / uni > thr;  // within 2^-20 of thr * union: the reference's quotient
+  return r;
 }
 
 // best class per anchor (first maximum, like torch.max): one thread per (image, anchor), all CUs
@@ -512,7 +527,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
       __syncthreads();
       uint32_t pre = 0, pmask = 0;
       int need = HEAD_CAP;
-#pragma unroll
+#pragma unroll 1
       for (int pass = 0; pass < 4; ++pass) {
         const int shift = 24 - 8 * pass;
         int* h = hist + 256 * (pass % 3);
