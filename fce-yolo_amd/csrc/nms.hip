@@ -816,8 +816,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
         __syncthreads();
         tick(0);
         if (!s_need) break;
-        // candidates entering the window: tested once against every box kept so far
-        const int Fn = min(Mg, F + win);
+        // candidates entering the window: tested once against every box kept so far.  Near max_det the step
+        // shrinks to what the survival rate so far (s_kept kept of F) says is still needed, +25 %, in multiples
+        // of 64: candidates past the greedy's stop are tested for nothing (any schedule gives the same result)
+        int step = win;
+        if (s_kept > 0 && stop != 12) {  // 12: diagnostics only (fixed steps)
+          const int64_t est = int64_t(max_det - s_kept) * F / s_kept;
+          step = min(win, max(64, int(((est * 5) / 4 + 63) & ~int64_t(63))));
+        }
+        const int Fn = min(Mg, F + step);
         for (int j = F + threadIdx.x; j < Fn; j += NMS_THREADS) lremoved[j] = 0;
         __syncthreads();
         test_range(F, Fn, 0, s_kept);

@@ -1,6 +1,6 @@
 """Phase timing of the device NMS on the bench workload (FCE_NMS_STOP=k ends the kernel after phase k: 1 candidates,
 2 the sorted-prefix select + 2048-slot sort, 10 the full 8192-slot sort instead, 5 the greedy without its window
-tests, 3 everything with the full sort, 0 the shipped kernel)."""
+tests, 3 everything with the full sort, 12 fixed frontier steps, 0 the shipped kernel)."""
 import os
 import sys
 from pathlib import Path
@@ -30,7 +30,7 @@ bsc, bcl = pred[:, 4:].max(1)
 for b in range(2):  # best-class spread of the candidates (how many kept boxes a candidate could share a class with)
     h = torch.bincount(bcl[b][bsc[b] > 0.25], minlength=eng.nc).sort(descending=True).values
     print(f"image {b}: classes used {int((h > 0).sum())}, largest class shares {(h[:4].float() / h.sum()).tolist()}")
-for stop in ("1", "2", "10", "5", "3", "0"):
+for stop in ("1", "2", "10", "5", "3", "12", "0"):
     os.environ["FCE_NMS_STOP"] = stop
     for _ in range(3):
         nms(pred)
