@@ -83,6 +83,8 @@ def hw_queues_env(argv, env):
     return "8" if lanes >= 4 and have < 8 else None
 
 
+_HWQ_GIVEN = os.environ.get("GPU_MAX_HW_QUEUES")  # as the caller set it (the N=1 line may raise it below)
+
 if __name__ == "__main__":
     _q = hw_queues_env(sys.argv[1:], os.environ)
     if _q is not None:
@@ -161,16 +163,28 @@ def parse_args():
                     help="batches in flight in the host-image legs (default predict.default_lanes: 5 on n / s, 3 on m / l)")
     ap.add_argument("--predict-steps", type=int, default=30,
                     help="batches of the host-image predict path timed after the main line (0 = skip)")
+    ap.add_argument("--dist-config-steps", type=int, default=None,
+                    help="N=1 only: also time this many steps in a child rank under the configuration `--gpus N` runs "
+                         "(a one-rank RCCL process group, its lanes and hardware queues, the per-batch all-gather) -> "
+                         "`value_dist_config` (default --steps; 0 = skip)")
+    ap.add_argument("--inputs", type=int, default=None,
+                    help="distinct resident input batches cycled through the timed steps (default lanes + 1, so no "
+                         "lane reads an input another lane has just pulled into the MALL)")
     ap.add_argument("--source", choices=("device", "host"), default="device",
                     help="device (default, the contract line): resident fp16 inputs; host: every rank predicts its "
                          "contiguous shard of decoded uint8 host images (dist.ShardedHostPredictor: H2D, letterbox, "
                          "forward, NMS, scale_boxes, per-batch gather of the detections) -- PCIe inclusive, not `value` "
                          "of the contract line")
     a = ap.parse_args()
+    a.lanes_given = a.lanes
     if a.lanes is None:
         a.lanes = default_lanes(a.model, os.environ, a.gpus)
     if a.graph < 0:
         a.graph = 1 if a.lanes > 1 else 0
+    if a.dist_config_steps is None:
+        a.dist_config_steps = a.steps
+    if a.inputs is None:
+        a.inputs = a.lanes + 1
     if a.predict_lanes is None:
         stem = Path(a.model).stem
         a.predict_lanes = 5 if (stem[6:7] if stem.startswith("yolo11") else "n") in ("n", "s") else 3
@@ -260,6 +274,46 @@ def cpu_baseline(model_name: str, imgsz: int, seconds: float, batch: int = 32):
     }
 
 
+def dist_config_line(a):
+    """`value_dist_config`: this N=1 workload timed again in a child process under exactly the configuration
+    `bench.py --gpus N` runs for N > 1 -- a one-rank RCCL process group (FCE_DIST_FORCE=1 under torch.distributed.run:
+    the weight broadcast, the per-batch packed all-gather on the side stream, max-over-ranks timing) with that
+    path's lanes and hardware queues (default_lanes / hw_queues_env decide them in the child as for any rank).  A
+    scaling ratio value(N) / (N x value(1)) otherwise folds the configuration change into "scaling" (DESIGN.md
+    §Multi-GPU).  The parent has released its lanes first; the child runs alone on the GPU."""
+    import subprocess
+
+    env = dict(os.environ, FCE_DIST_FORCE="1")
+    if _HWQ_GIVEN is None:
+        env.pop("GPU_MAX_HW_QUEUES", None)
+    else:
+        env["GPU_MAX_HW_QUEUES"] = _HWQ_GIVEN
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), "--gpus", "1",
+           "--steps", str(a.dist_config_steps), "--warmup", str(a.warmup), "--model", a.model, "--batch", str(a.batch),
+           "--imgsz", str(a.imgsz), "--cpu-seconds", "0", "--predict-steps", "0", "--profile-passes", "1",
+           "--dist-config-steps", "0"]
+    if a.lanes_given is not None:  # an explicit --lanes is what the --gpus N ranks would run too
+        cmd += ["--lanes", str(a.lanes_given)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    line = next((ln for ln in reversed(r.stdout.splitlines()) if ln.startswith("{")), None)
+    if r.returncode != 0 or line is None:
+        return {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+    d = json.loads(line)
+    c = d["config"]
+    return {"value": d["value"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+            "batches_in_flight": c["batches_in_flight"], "hw_queues": c["hw_queues"],
+            "process_group": d["process_group"],
+            "note": "N=1 under the --gpus N configuration (one-rank RCCL group, per-batch all-gather); the 1-GPU point "
+                    "of a scaling curve compares like with like against this value"}
+
+
 def host_source_line(a, model, rank, world, use_dist, dev):
     """--source host: the sharded host-image path, one JSON line (PCIe inclusive)."""
     import numpy as np
@@ -267,7 +321,8 @@ def host_source_line(a, model, rank, world, use_dist, dev):
     from fce_yolo_amd.dist import ShardedHostPredictor
 
     B, S = a.batch, a.imgsz
-    sp = ShardedHostPredictor(model, B * world, S, dev, batch_size=B, lanes=a.predict_lanes, workers=4)
+    sp = ShardedHostPredictor(model, B * world, S, dev, batch_size=B, lanes=a.predict_lanes, workers=4,
+                              gather=use_dist)
     # each rank decodes (synthesises) only its own shard: image i of a global batch is seeded by i
     shard = [np.random.default_rng(i).integers(0, 256, (480, 640, 3), dtype=np.uint8) for i in range(sp.start, sp.end)]
 
@@ -360,16 +415,23 @@ def main():
     eng = sp.engine
     for e in sp.pipe.engs:
         e.graph = bool(a.graph)
-    x = torch.rand(B, 3, S, S, generator=torch.Generator().manual_seed(1000 + rank)).half().to(dev)
+    # a ring of distinct resident input batches (lanes + 1 by default), cycled by the steps: no lane re-reads an input
+    # batch another lane has just pulled through the 256 MB MALL
+    gen = torch.Generator().manual_seed(1000 + rank)
+    xs = [torch.rand(B, 3, S, S, generator=gen).half().to(dev) for _ in range(max(1, a.inputs))]
+    x = xs[0]
     nms = NMS(B, eng.anchors, eng.nc, dev)
+    it = [0]
 
     def step():
+        xi = xs[it[0] % len(xs)]
+        it[0] += 1
         if a.no_nms:
-            eng(x)
+            eng(xi)
         elif a.sequential:
-            nms(eng(x), eng.best)
+            nms(eng(xi), eng.best)
         else:  # forward of this batch overlaps the NMS (+ multi-GPU gather) of the previous one
-            sp.submit(x)
+            sp.submit(xi)
 
     def barrier():
         if use_dist:
@@ -490,6 +552,7 @@ def main():
         "config": {"workload": f"{stem} detection inference (forward + decode + NMS) @ {S}x{S}, {B} images/GPU",
                    "model": stem, "global_batch": B * world, "imgsz": S, "parallelism": f"dp{world}",
                    "batches_in_flight": 1 if (a.no_nms or a.sequential) else a.lanes,
+                   "distinct_inputs": len(xs),
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                    "forward_launch": "hipgraph" if a.graph else "direct"},
         "roofline": roof,
@@ -513,11 +576,15 @@ def main():
     }
     if a.profile_json and rank == 0:
         Path(a.profile_json).write_text(json.dumps([list(p) for p in prof], indent=0))
-    if rank == 0 and world == 1 and a.predict_steps > 0:
-        # the main line's lanes (executors, streams, arenas) are released first: the predict path brings its own
+    if rank == 0 and world == 1 and (a.predict_steps > 0 or a.dist_config_steps > 0):
+        # the main line's lanes (executors, streams, arenas) are released first: the later legs bring their own
         sp.close()
         sp = eng = nms = None
+        xs = x = None
         torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and a.dist_config_steps > 0 and not use_dist and not (a.no_nms or a.sequential):
+        out["value_dist_config"] = dist_config_line(a)
+    if rank == 0 and world == 1 and a.predict_steps > 0:
         out["predict_pcie_inclusive"] = predict_rate(model, B, S, dev, a.predict_steps, a.predict_lanes)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.model, S, a.cpu_seconds, B)

@@ -1233,10 +1233,14 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
     for (int i = 0; i < NL; ++i) tile[cur * BUF + ss[i]] = vv[i];
     __syncthreads();
     const int tx = t % tiles_x, r0 = t / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
-    if (t + PD * step < tend) stage_load(t + PD * step, vv, ss);
-    f4 acc[1][RP];
+    Tile3Pre<RP> pre;  // residual + bias, issued before the prefetch (see tile3_pre)
+    tile3_pre<RP>(a, n, ty * TH, tx * TW, cot0, grp, col, pre);
+    // unconditional (clamped to the last tile, whose loads are then unused): a prefetch under a branch leaves the
+    // waitcnt pass a join with nothing in flight on one side, and it waits vmcnt(0) for the residual there
+    stage_load(min(t + PD * step, tend - 1), vv, ss);
+    f4 acc[RP];
 #pragma unroll
-    for (int p = 0; p < RP; ++p) acc[0][p] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < RP; ++p) acc[p] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
 #pragma unroll
@@ -1246,10 +1250,10 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
         for (int p = 0; p < RP; ++p) {
           const int u = (p * S + ky) * CI + tile_col<S, CI>(col * S + kx);
           const h8 bf = tile[cur * BUF + u * NQ + tile_slot<KP>(u, k * 4 + grp)];
-          acc[0][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k * 9 + tap], bf, acc[0][p], 0, 0, 0);
+          acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k * 9 + tap], bf, acc[p], 0, 0, 0);
         }
       }
-    tile3_store<1, RP>(a, acc, n, ty * TH, tx * TW, cot0, col, grp);
+    tile3_post<RP>(a, acc, pre, n, ty * TH, tx * TW, cot0, col, grp);
     t += step;
   };
   stage_load(t, v, sl);

@@ -139,6 +139,70 @@ __device__ __forceinline__ void tile3_store(const ConvArgs& a, f4 (&acc)[RC][RP]
   }
 }
 
+// The same epilogue split in two for the persistent 3x3 ring (one cout tile per wave): tile3_pre loads the
+// residuals and biases of the wave's tile (clamped, unconditional) BEFORE the next tile's staging loads are issued,
+// so tile3_post needs no vmcnt(0): vmcnt retires in issue order, and a wait for a residual issued after the
+// prefetch waited for the whole prefetch (the ring's look-ahead was lost at every epilogue).
+template <int RP>
+struct Tile3Pre {
+  h4 r[RP];
+  float bz[4];
+};
+
+template <int RP>
+__device__ __forceinline__ void tile3_pre(const ConvArgs& a, int n, int oy0, int ox0, int cot0, int grp, int col,
+                                          Tile3Pre<RP>& pre) {
+  const int co0 = min(cot0 * 16 + grp * 4, (a.cout - 4) & ~3);
+  const int ox = min(ox0 + col, a.Wo - 1);
+  if (a.res && a.vec_ok && a.cout >= 4) {
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int64_t pix = (int64_t(n) * a.Ho + min(oy0 + p, a.Ho - 1)) * a.Wo + ox;
+      pre.r[p] = *reinterpret_cast<const h4*>(a.res + pix * a.rcs + co0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pre.bz[j] = bias_or0(a.bias, cot0 * 16 + grp * 4 + j, a.cout);
+}
+
+template <int RP>
+__device__ __forceinline__ void tile3_post(const ConvArgs& a, f4 (&acc)[RP], const Tile3Pre<RP>& pre, int n, int oy0,
+                                           int ox0, int cot0, int col, int grp) {
+  const int ox = ox0 + col;
+  const int co0 = cot0 * 16 + grp * 4;
+  if (ox >= a.Wo || cot0 >= ((a.cout + 15) >> 4) || co0 >= a.cout) return;
+  const bool vec = a.vec_ok && co0 + 3 < a.cout;
+#pragma unroll
+  for (int p = 0; p < RP; ++p) {
+    const int oy = oy0 + p;
+    if (oy >= a.Ho) continue;
+    const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float tt = acc[p][j] + pre.bz[j];
+      v[j] = a.act ? silu(tt) : tt;
+    }
+    _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
+    if (a.res) {
+      if (vec && a.cout >= 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)pre.r[p][j]);
+      } else {
+        const _Float16* ro = a.res + pix * a.rcs + co0;
+        for (int j = 0; j < 4; ++j)
+          if (co0 + j < a.cout) v[j] = fpin(v[j] + (float)ro[j]);
+      }
+    }
+    if (vec) {
+      *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (co0 + j < a.cout) yo[j] = (_Float16)fpin(v[j]);
+    }
+  }
+}
+
 // Epilogue of the dense MFMA kernels: acc[r][p] = 16 couts (cout tile cot0 + r) x 16 pixels
 // (pix_base + 16 p ..) of this wave; lane = (col = pixel, grp = 4-cout group).  Bias, SiLU, residual,
 // BiFPN weighted store / accumulate, or the fused Detect DFL / cls-sigmoid tails.

@@ -68,6 +68,15 @@ struct C3k2Args {
   int diag;           // FCE_C3K2_DIAG: block 0 prints its per-stage clocks
 };
 
+// Barrier between the stages of one tile: the LDS writes published (lgkmcnt(0)), the global traffic left in flight
+// (__syncthreads() also waits vmcnt(0), i.e. for the next tile's x prefetch at the barrier after stage 1 and for
+// the tile's y stores at its end; measured the same either way, round 5, the kernel's time being its stage chain)
+__device__ __forceinline__ void c3_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ h4 c3_h4(const float (&v)[4]) {
   return h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
 }
@@ -226,7 +235,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
     tick(0);
     if (t + 1 < t_end) load_x(t + 1);  // in flight during stages 2-4
     tick(1);
-    __syncthreads();
+    c3_barrier();
     // ---------------- stage 2: h = m.cv1(b) over the m.cv1 region (3x3 from the t image)
     {
       int pb[G::MF2];
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
       c3_stage<G::MF2, G::CT2, G::NS2>(sm + G::OW2 + lane, bl, epi);
     }
     tick(2);
-    __syncthreads();
+    c3_barrier();
     // ---------------- stage 3: m = m.cv2(h) + b over the tile (3x3 from the h image)
     {
       int pb[G::MF4];
@@ -289,7 +298,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
       c3_stage<G::MF4, G::CT3, G::NS3>(sm + G::OW3 + lane, bl, epi);
     }
     tick(3);
-    __syncthreads();
+    c3_barrier();
     // ---------------- stage 4: y = cv2([a | b | m]) over the tile, to HBM
     {
       int pt[G::MF4], pm[G::MF4];
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
       c3_stage<G::MF4, G::CT4, G::NS4>(sm + G::OW4 + lane, bl, epi);
     }
     tick(4);
-    __syncthreads();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
+    c3_barrier();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
     tick(5);
   }
   if (a.diag && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -367,13 +376,18 @@ static int c3_launch(const C3k2Args& a0, int H, int W, int N, hipStream_t s) {
   return launch_status("c3k2_fused_kernel");
 }
 
-// FCE_C3K2_TILE="8,16,4" / "4,40,8" forces one of the two tiles (tests, tuning); otherwise by map width
+// FCE_C3K2_TILE="8,16,4" / "4,40,8" forces one of the two tiles (tests, tuning); otherwise by map width.  Any other
+// value is an error (it once fell back to the choice by width silently).  Round 5 measured 16x16 (4 or 8 waves),
+// 8x32, 4x40 with 4 waves and a y tile staged through LDS for 16-byte stores: none faster
 template <int CIN, int C, int CM, int COUT>
 static int c3_launch_cfg(const C3k2Args& a, int H, int W, int N, hipStream_t s) {
   const char* env = getenv("FCE_C3K2_TILE");  // read per call: tests switch it within one process
   bool wide = W >= 128;
-  if (env && strcmp(env, "8,16,4") == 0) wide = true;
-  if (env && strcmp(env, "4,40,8") == 0) wide = false;
+  if (env && *env) {
+    if (strcmp(env, "8,16,4") == 0) wide = true;
+    else if (strcmp(env, "4,40,8") == 0) wide = false;
+    else return fail(FCE_ERR_INVALID, "FCE_C3K2_TILE: only \"8,16,4\" or \"4,40,8\"");
+  }
   return wide ? c3_launch<CIN, C, CM, COUT, 8, 16, 4>(a, H, W, N, s) : c3_launch<CIN, C, CM, COUT, 4, 40, 8>(a, H, W, N, s);
 }
 

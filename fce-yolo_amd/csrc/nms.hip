@@ -505,7 +505,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const float* pred, con
   if (tiled && stop != 3 && stop != 10) {
     hn = ncand;
     head = hn <= HEAD_CAP && hn > 0;
-    if (!head && hn <= RADIX_CAP) {
+    if (hn > HEAD_CAP && hn <= RADIX_CAP) {  // empty and small sets never reach the select
       // ---- 2s. more than HEAD_CAP candidates: only the first HEAD_CAP entries of the sorted order (score desc,
       // position asc) are sorted.  A radix select (four 8-bit digit passes over the score bits held in registers,
       // wave-aggregated LDS atomics, three rotating histograms so each pass has one barrier, every wave finding

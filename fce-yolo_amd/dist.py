@@ -5,6 +5,8 @@
   lowest ranks, and a batch size >= the dataset degenerating to batch size 1.
 * `broadcast_module` sends rank 0's weights to every rank once per model load (RCCL over xGMI on the
   GPU box, gloo on CPU).
+* `DeviceGather` is the per-batch collective of both sharded predictors: one packed all-gather of the NMS
+  outputs on a side stream (RCCL over xGMI), issued in batch order.
 * `gather_detections` collects every rank's post-NMS detections on all ranks (variable sizes, host sync).
 * `ShardedPredictor` is the per-step multi-GPU entry point (`bench.py --gpus N`): rank r runs its
   contiguous shard of each global batch through Engine + Pipeline, and the packed post-NMS outputs of
@@ -113,6 +115,51 @@ def unpack_gathered(gathered: torch.Tensor, sizes: list[int], max_det: int):
     return dets, keep
 
 
+class DeviceGather:
+    """One packed all-gather of a batch's NMS outputs (``engine.NMS`` layout: keep | dets | counts) per batch, on the
+    device: every rank sends its shard padded to the largest shard's layout (a remainder shard is re-packed into
+    a per-slot send buffer), RCCL's ``all_gather_into_tensor`` writes the ranks' blocks in rank order, and
+    ``unpack`` cuts the host copy into per-image results in the unsharded order.  The caller issues it on one
+    side stream in batch order, so every rank's collectives come in the same order (the reference gathers
+    validation results to rank 0 with gather_object, models/yolo/detect/val.py:222-241, through the host).
+    With gloo (CPU rehearsals of the GPU path) the send block goes through host memory."""
+
+    def __init__(self, sizes: list[int], rank: int, max_det: int):
+        from .engine import NMS
+
+        self.sizes, self.rank, self.max_det = list(sizes), rank, max_det
+        self.world, self.batch, self.bmax = len(sizes), sizes[rank], max(sizes)
+        self.nb = NMS.packed_bytes(self.bmax, max_det)
+        self.nbytes = self.world * self.nb  # gathered bytes per batch
+        self.nccl = dist.get_backend() == "nccl"
+
+    def buffers(self, device):
+        """(send or None, gathered) device buffers for one in-flight slot."""
+        send = torch.zeros(self.nb, dtype=torch.uint8, device=device) if self.batch < self.bmax else None
+        return send, torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+
+    def issue(self, nms, send, gathered):
+        """Gather slot `nms`'s outputs into `gathered` on the current stream."""
+        from .engine import NMS
+
+        src = nms.buf
+        if send is not None:  # a remainder shard: re-pack into the bmax layout every rank sends
+            keep, dets, counts = NMS.unpack(send, self.bmax, self.max_det)
+            keep[: self.batch].copy_(nms.keep)
+            dets[: self.batch].copy_(nms.dets)
+            counts[: self.batch].copy_(nms.counts)
+            src = send
+        if self.nccl or src.device.type == "cpu":
+            dist.all_gather_into_tensor(gathered, src)
+        else:
+            out = torch.empty(self.nbytes, dtype=torch.uint8)
+            dist.all_gather_into_tensor(out, src.cpu())
+            gathered.copy_(out)
+
+    def unpack(self, host: torch.Tensor):
+        return unpack_gathered(host, self.sizes, self.max_det)
+
+
 class ShardedPredictor:
     """Batch-sharded detection inference, one process per GPU.
 
@@ -143,26 +190,15 @@ class ShardedPredictor:
         self.max_det = nms_kw.get("max_det", 300)
         lanes = max(1, int(lanes))
         depth = -(-max(depth, lanes) // lanes) * lanes  # Pipeline's slot count
-        nb = NMS.packed_bytes(self.bmax, self.max_det)
         # each rank's packed outputs padded to bmax images, so every rank contributes the same bytes
-        self.send = [torch.zeros(nb if self.batch < self.bmax else 0, dtype=torch.uint8, device=device)
-                     for _ in range(depth)]
-        self.gathered = [torch.zeros(self.world * nb if self.do_gather else 0, dtype=torch.uint8, device=device)
-                         for _ in range(depth)]
+        self.gather = DeviceGather(self.sizes, self.rank, self.max_det) if self.do_gather else None
+        bufs = [self.gather.buffers(device) for _ in range(depth)] if self.do_gather else []
+        self.send = [b[0] for b in bufs]
+        self.gathered = [b[1] for b in bufs]
         self.pipe = Pipeline(self.engine, depth, post=self._gather if self.do_gather else None, lanes=lanes, **nms_kw)
 
     def _gather(self, k: int):
-        from .engine import NMS
-
-        nms = self.pipe.nms[k]
-        send = nms.buf
-        if self.batch < self.bmax:  # a remainder shard: re-pack into the bmax layout every rank sends
-            send = self.send[k]
-            keep, dets, counts = NMS.unpack(send, self.bmax, self.max_det)
-            keep[: self.batch].copy_(nms.keep)
-            dets[: self.batch].copy_(nms.dets)
-            counts[: self.batch].copy_(nms.counts)
-        dist.all_gather_into_tensor(self.gathered[k], send)
+        self.gather.issue(self.pipe.nms[k], self.send[k], self.gathered[k])
 
     def submit(self, x: torch.Tensor) -> int:
         if x.shape[0] != self.batch:
@@ -180,7 +216,7 @@ class ShardedPredictor:
             self.pipe.flush()
         self.pipe.nms_done[k].synchronize()
         if self.do_gather:
-            return unpack_gathered(self.gathered[k], self.sizes, self.max_det)
+            return self.gather.unpack(self.gathered[k])
         # no collective: this rank's own images only (its shard, in order)
         return unpack_gathered(self.pipe.nms[k].buf, [self.batch], self.max_det)
 
@@ -214,7 +250,12 @@ class ShardedHostPredictor:
     detections of every rank are all-gathered once per batch (fixed-size packed tensors: RCCL over xGMI on the
     device for the nccl backend, host tensors for gloo), so `stream` yields each global batch's results in the
     unsharded image order on every rank -- what one Predictor over the whole batch returns.  Images never cross
-    GPUs; only ~7 KB of detections per image do."""
+    GPUs; only ~7 KB of detections per image do.
+
+    With the real Predictor the gather is device-side and asynchronous (`DeviceGather`): each batch's packed NMS
+    outputs are all-gathered on the predictor's side stream, in batch order, right behind the batch's scale_boxes,
+    and the ONE D2H copy of the batch brings the gathered block back, so the submit loop never waits on a
+    collective.  A custom `predictor` (tests' host stubs) gets the host gather of its per-image results."""
 
     def __init__(self, model, total: int, imgsz, device, batch_size: int | None = None, lanes: int | None = None,
                  gather: bool | None = None, predictor=None, max_det: int = 300, **kw):
@@ -233,10 +274,12 @@ class ShardedHostPredictor:
             raise ValueError(f"empty shard(s) {self.sizes} of a {total}-image batch over {self.world} ranks")
         self.bmax = max(self.sizes)
         self.max_det = max_det
+        self.device_gather = predictor is None and self.do_gather
         if predictor is None:
             from .predict import Predictor
 
-            self.pred = Predictor(model, self.batch, imgsz, device, lanes=lanes, max_det=max_det, **kw)
+            g = DeviceGather(self.sizes, self.rank, max_det) if self.device_gather else None
+            self.pred = Predictor(model, self.batch, imgsz, device, lanes=lanes, max_det=max_det, gather=g, **kw)
         else:
             self.pred = predictor(self.batch)
         backend = dist.get_backend() if dist.is_initialized() else "gloo"
@@ -252,7 +295,7 @@ class ShardedHostPredictor:
         return list(images[self.start:self.end])
 
     def _gather(self, dets, keep):
-        if not self.do_gather:
+        if not self.do_gather or self.device_gather:
             return dets, keep
         packed = [t.to(self.comm_device) for t in pack_detections(dets, keep, self.bmax, self.max_det)]
         outs = []

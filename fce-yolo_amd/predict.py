@@ -97,6 +97,7 @@ class _Lane:
         self.best = eng.new_best()
         self.nms = NMS(batch, eng.anchors, eng.nc, device, **nms_kw)
         self.out_host = torch.empty(self.nms.buf.numel(), dtype=torch.uint8, pin_memory=True)
+        self.send = self.gathered = None  # the multi-GPU gather's buffers (Predictor(gather=...))
         self.done = torch.cuda.Event()
         self.ticket = None  # ticket whose results this lane holds (not yet collected)
         self.shapes = []
@@ -157,13 +158,17 @@ class Predictor:
     last canvas (those rows are dropped).  `__call__` = result(submit(...))."""
 
     def __init__(self, model, batch: int, imgsz=640, device=None, conf=0.25, iou=0.7, max_det=300,
-                 lanes: int | None = None, graph: bool = True, workers: int | None = None, copy_stream: bool = True):
+                 lanes: int | None = None, graph: bool = True, workers: int | None = None, copy_stream: bool = True,
+                 gather=None):
         """`lanes`: batches on the device at once; default by scale (`default_lanes`): 5 on the n / s scales
         (measured best for 32 x 480x640 images, scripts/predict_diag.py), 3 on m / l, where every lane's
         activation arena is large and more than three arenas overflow the MALL (bench.default_lanes).
         `workers`: host threads packing images into pinned memory (default min(8, cpus / 2); 4-8 reach ~31 GB/s
         on the MI355X box).  `copy_stream` (default): every H2D copy on one dedicated stream, lanes wait on it
-        (18.9k against 15.9k images/s with the copy on the lane's own stream, scripts/predict_diag.py)."""
+        (18.9k against 15.9k images/s with the copy on the lane's own stream, scripts/predict_diag.py).
+        `gather` (a `dist.DeviceGather`, set by dist.ShardedHostPredictor): every batch's packed NMS outputs are
+        all-gathered over the ranks on one side stream in batch order before the D2H copy, and results are the
+        whole global batch's (every submit must then carry exactly `batch` images)."""
         import os
         from concurrent.futures import ThreadPoolExecutor
 
@@ -178,6 +183,13 @@ class Predictor:
         for e in engs:
             e.graph = graph
         self.lanes = [_Lane(e, batch, self.device, nms_kw) for e in engs]
+        self.gather = gather
+        self.comm = None
+        if gather is not None:
+            self.comm = torch.cuda.Stream(self.device)  # the collectives, in batch order
+            for ln in self.lanes:
+                ln.send, ln.gathered = gather.buffers(self.device)
+                ln.out_host = torch.empty(gather.nbytes, dtype=torch.uint8, pin_memory=True)
         self.copy = torch.cuda.Stream(self.device) if copy_stream else None
         self.stages = [_Stage() for _ in range(len(self.lanes) + 1)]
         self.nms = self.lanes[0].nms  # lane 0's NMS (API compatibility)
@@ -197,6 +209,8 @@ class Predictor:
         Returns the record _issue consumes; the packing runs while the caller does other work."""
         if not 0 < len(images) <= self.batch:
             raise ValueError(f"Predictor: 1..{self.batch} images per call")
+        if self.gather is not None and len(images) != self.batch:
+            raise ValueError(f"Predictor: the gathered path takes whole {self.batch}-image shards, got {len(images)}")
         imgs = [_host_image(im) for im in images]
         for im in imgs:
             if im.dtype != np.uint8 or im.ndim != 3 or im.shape[2] != 3:
@@ -275,7 +289,16 @@ class Predictor:
             dets, keep, counts = ln.nms(ln.pred, ln.best)
             N.call("fce_scale_boxes", C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()), self.batch,
                    self.max_det, C.c_void_p(sc.data_ptr()), st)
-            ln.out_host.copy_(ln.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
+            if self.gather is None:
+                ln.out_host.copy_(ln.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
+        if self.gather is not None:  # every rank's packed outputs (side stream, batch order), then one D2H copy
+            self.comm.wait_stream(ln.stream)
+            with torch.cuda.stream(self.comm):
+                self.gather.issue(ln.nms, ln.send, ln.gathered)
+            ln.stream.wait_stream(self.comm)
+            with torch.cuda.stream(ln.stream):
+                ln.out_host.copy_(ln.gathered, non_blocking=True)
+        with torch.cuda.stream(ln.stream):
             ln.done.record(ln.stream)
         ln.ticket = i + 1
         ln.shapes = shapes
@@ -291,6 +314,9 @@ class Predictor:
 
     def _collect(self, ln: _Lane):
         ln.done.synchronize()
+        if self.gather is not None:
+            ln.ticket = None
+            return self.gather.unpack(ln.out_host.clone())  # the whole global batch, unsharded order
         keep, dets, counts = NMS.unpack(ln.out_host.clone(), self.batch, self.max_det)  # one copy out of pinned memory
         n = len(ln.shapes)
         cnt = counts[:n].tolist()

@@ -52,10 +52,10 @@ case "$CMD" in
     shift
     pytest_gpu "$OUT/pytest.log" -k "$K"
     rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-    bench_line "$OUT/bench.log" --steps 30 --warmup 5 --cpu-seconds 0 --predict-steps 0 --profile-json "$OUT/profile.json" "$@"
+    bench_line "$OUT/bench.log" --steps 30 --warmup 5 --cpu-seconds 0 --predict-steps 0 --dist-config-steps 0 --profile-json "$OUT/profile.json" "$@"
     ;;
   bench)
-    bench_line "$OUT/bench.log" --cpu-seconds 0 --predict-steps 0 --profile-json "$OUT/profile.json" "$@"
+    bench_line "$OUT/bench.log" --cpu-seconds 0 --predict-steps 0 --dist-config-steps 0 --profile-json "$OUT/profile.json" "$@"
     ;;
   env)
     i=0
@@ -63,7 +63,7 @@ case "$CMD" in
       for setting in "$@"; do
         i=$((i + 1))
         echo -n "[$setting] "
-        env $setting timeout -k 10 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 0 --predict-steps 0 \
+        env $setting timeout -k 10 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 0 --predict-steps 0 --dist-config-steps 0 \
           --profile-passes 3 $BARGS > "$OUT/env$i.log" 2>&1
         rc=$?
         echo "rc=$rc $(grep -o '"value": [0-9.]*\|"forward_ms_per_batch": [0-9.]*\|"value_1lane": [0-9.]*' "$OUT/env$i.log" | tr '\n' ' ')"
@@ -82,7 +82,7 @@ case "$CMD" in
       t=$1
       shift
       echo -n "$t "
-      bench_line "$OUT/$t.log" --steps 30 --warmup 5 --cpu-seconds 0 --predict-steps 0 "$@" || exit $?
+      bench_line "$OUT/$t.log" --steps 30 --warmup 5 --cpu-seconds 0 --predict-steps 0 --dist-config-steps 0 "$@" || exit $?
     done
     ;;
   prof)

@@ -10,7 +10,7 @@ shift
 pass() {
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d gpurun_out/pmc/${TAG}_$name -o run -- \
-    python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --predict-steps 0 --profile-passes 1 --no-nms \
+    python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --predict-steps 0 --dist-config-steps 0 --profile-passes 1 --no-nms \
     --profile-json gpurun_out/pmc/${TAG}_profile_$name.json $BARGS > gpurun_out/pmc/${TAG}_$name.log 2>&1
   local rc=$?; echo "pmc $name rc=$rc"; return $rc
 }

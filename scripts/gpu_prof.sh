@@ -9,7 +9,7 @@ TAG=${1:-r01}
 shift
 STEPS=20
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/$TAG -o run -- \
-  python bench.py --steps $STEPS --warmup 5 --cpu-seconds 0 "$@" > gpurun_out/prof/${TAG}_bench.log 2>&1
+  python bench.py --steps $STEPS --warmup 5 --cpu-seconds 0 --dist-config-steps 0 "$@" > gpurun_out/prof/${TAG}_bench.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof/${TAG}_bench.log
 [ $rc -eq 0 ] || exit $rc
 python scripts/trace_summary.py gpurun_out/prof/$TAG $STEPS gpurun_out/prof/${TAG}_bench.log > gpurun_out/prof/${TAG}_trace_summary.json

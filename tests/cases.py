@@ -208,6 +208,44 @@ E2E_NMS640 = {
 }
 
 
+E2E_NMS_ML = {
+    # fixture key: (cfg, -h8 BiCoordCrossAtt heads, batch, imgsz) -- make_golden_e2e_nms_ml.CASES: designed classes on
+    # all three Detect levels; l-fce 640 (the per-rank shard scale of the 8-GPU l256 config), m-fce-h8 1280 (config 4)
+    "yolo11n-fce_640_b8_3lvl": ("yolo11n-fce.yaml", False, 8, 640),
+    "yolo11l-fce_640_b2_3lvl": ("yolo11l-fce.yaml", False, 2, 640),
+    "yolo11m-fce-h8_1280_b2_3lvl": ("yolo11m-fce.yaml", True, 2, 1280),
+}
+
+
+def designed_model_ml(key, fx):
+    """(model, input) of an all-levels margin-designed case (make_golden_e2e_nms_ml.py)."""
+    import re
+
+    from fce_yolo_amd.parser import DetectionModel, load_cfg
+
+    cfg, h8, b, s = E2E_NMS_ML[key]
+    d = load_cfg(cfg)
+    if h8:
+        for row in d["backbone"]:
+            if row[2] == "BiCoordCrossAtt":
+                row[3] = [512, 8, 8]
+    model = DetectionModel(d)
+    sd = seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0, gain=float(fx["gain"]))
+    det = len(model.model) - 1
+    n = 0
+    for k in sd:
+        m = re.match(rf"^model\.{det}\.cv3\.(\d+)\.2\.(weight|bias)$", k)
+        if m:
+            sd[k] = torch.from_numpy(fx[f"cls_{m.group(2)[0]}{m.group(1)}"].copy())
+            n += 1
+    assert n == 6, n
+    model.load_state_dict(sd)
+    seeds = [int(v) for v in fx["seeds"]]
+    assert len(seeds) == b
+    x = torch.cat([torch.rand(1, 3, s, s, generator=torch.Generator().manual_seed(v)) for v in seeds])
+    return model.eval(), x
+
+
 def designed_model640(key, fx):
     """(model, input) of a headline-size margin-designed case (make_golden_e2e_nms640.py): the designed Detect cls
     convs on seeded_state_dict(keys, 0, gain), and the batch of per-image seeded inputs."""

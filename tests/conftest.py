@@ -63,6 +63,11 @@ def e2e_nms640_fx():
 
 
 @pytest.fixture(scope="session")
+def e2e_nms_ml_fx():
+    return _Npz(GOLDEN / "e2e_nms_ml.npz")
+
+
+@pytest.fixture(scope="session")
 def nms_fx():
     return _Npz(GOLDEN / "nms.npz")
 

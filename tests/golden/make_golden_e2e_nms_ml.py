@@ -1,0 +1,207 @@
+"""Margin-designed END-TO-END NMS fixtures over ALL THREE Detect levels, and at the l and m scales, from the
+REFERENCE (build container only).
+
+    python tests/golden/make_golden_e2e_nms_ml.py [case ...]
+
+make_golden_e2e_nms640.py designs one level (20 x 20) of the n / s heads.  These cases put candidates on every
+level of one image, so the HIP forward's P3 / P4 / P5 outputs all reach the device NMS with indices the
+reference fixes, and cover the scales of the multi-GPU configuration (l-fce 640, whose per-rank l32 shard is the
+8-GPU l256 config) and BASELINE config 4 (m-fce + BiCoordCrossAtt(num_heads=8) at 1280):
+
+  * every level i carries its own NCLS_L designed classes (level 0: classes 0..2, level 1: 3..5, level 2: 6..7):
+    they read the top principal directions of THAT level's cls features over a calibration batch, standardised
+    and scaled by K; every other (level, class) gets weight 0 and bias -30;
+  * each level's offset targets TARGET candidates per image on that level (median over the calibration batch);
+  * per image, input seeds are searched until the reference fp32 output meets make_golden_e2e_nms.margins (every
+    candidate score gap and distance from conf > 1e-2, no same-class IoU within 2e-2 of iou_thres), and at
+    least one candidate sits on every level (`_levels_ok`);
+  * the whole batch is re-run at its real batch size and re-checked, then the reference's non_max_suppression
+    (utils/nms.py:13-166, TorchNMS :239-296, return_idxs=True) gives the stored kept indices and rows.
+
+Stored per case (npz key prefix = case): seeds, gain, designed cls weights per level, keep{b} / det{b}, and
+y_cand{b}: the reference's rows 0..4+NCLS-1 at that image's candidate anchors (cand{b}) for the score / box
+error report.  Inputs are torch.rand(1, 3, S, S, manual_seed(seed_b)) per image; the rest of the weights are
+seeded_state_dict(keys, 0, gain).  Same import recipe as make_golden.py; the -h8 variant edits the YAML's
+BiCoordCrossAtt args to [512, 8, 8] as bench.model_cfg does.
+"""
+
+from __future__ import annotations
+
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+import make_golden  # noqa: E402
+import make_golden_e2e_nms as E  # noqa: E402
+
+CONF, IOU, MAX_DET = E.CONF, E.IOU, E.MAX_DET
+LEVEL_CLASSES = ([0, 1, 2], [3, 4, 5], [6, 7])
+NCLS = 8
+K = 3.0
+SEEDS_PER_IMAGE = 600
+
+# key: (yaml, h8, batch, imgsz, seed base, seeded_state_dict gain, target candidates per image per level)
+CASES = {
+    "yolo11n-fce_640_b8_3lvl": ("yolo11n-fce.yaml", False, 8, 640, 650_000, 1.45, 1.5),
+    "yolo11l-fce_640_b2_3lvl": ("yolo11l-fce.yaml", False, 2, 640, 651_000, 1.2, 1.5),
+    "yolo11m-fce-h8_1280_b2_3lvl": ("yolo11m-fce.yaml", True, 2, 1280, 652_000, 1.25, 1.5),
+}
+
+
+def image(seed, s):
+    return torch.rand(1, 3, s, s, generator=torch.Generator().manual_seed(seed))
+
+
+def level_ranges(s):
+    """[(a0, a1)] anchor ranges of the three levels (strides 8, 16, 32)."""
+    out, a = [], 0
+    for st in (8, 16, 32):
+        n = (s // st) ** 2
+        out.append((a, a + n))
+        a += n
+    return out
+
+
+def _levels_ok(y, s):
+    """Every image has at least one candidate on every level."""
+    for b in range(y.shape[0]):
+        sc = y[b, 4:].max(0)
+        for a0, a1 in level_ranges(s):
+            if not (sc[a0:a1] > CONF).any():
+                return False
+    return True
+
+
+def _search(model, s, first, bi, per_fwd):
+    t0 = time.time()
+    for j in range(0, SEEDS_PER_IMAGE, per_fwd):
+        xs = [first + j + u for u in range(per_fwd)]
+        with torch.inference_mode():
+            y = model(torch.cat([image(sx, s) for sx in xs]))[0].numpy()
+        for u, sx in enumerate(xs):
+            yu = y[u:u + 1]
+            if E.margins(yu)[0] and _levels_ok(yu, s):
+                print(f"  image {bi}: seed {sx} after {j + u + 1} tries, {time.time() - t0:.1f}s", flush=True)
+                return sx, j + u + 1
+    return None, SEEDS_PER_IMAGE
+
+
+def build(tasks, key):
+    from fce_yolo_amd.weights import seeded_state_dict
+
+    yaml_name, h8, bs, s, seed0, gain, target = CASES[key]
+    d = tasks.yaml_model_load(str(E.CFG / yaml_name))
+    if h8:
+        for row in d["backbone"]:
+            if row[2] == "BiCoordCrossAtt":
+                row[3] = [512, 8, 8]
+    model = tasks.DetectionModel(d, ch=3, verbose=False)
+    base = seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], seed=0, gain=gain)
+    det_idx = len(model.model) - 1
+    nl = len(E.cls_keys(base, det_idx)) // 2
+    assert nl == 3
+    model.load_state_dict(base)
+    model.eval()
+    xc = torch.cat([image(seed0 - 1 - i, s) for i in range(4)])
+    feats = {}
+    hooks = [model.model[-1].cv3[i][2].register_forward_hook(
+        lambda m, a, o, i=i: feats.__setitem__(i, a[0].detach().double())) for i in range(nl)]
+    with torch.inference_mode():
+        model(xc)
+    for h in hooks:
+        h.remove()
+    sd = dict(base)
+    zs = []
+    for i in range(nl):
+        f = feats[i].permute(0, 2, 3, 1).reshape(-1, feats[i].shape[1])
+        cls = LEVEL_CLASSES[i]
+        _, evecs = torch.linalg.eigh(torch.cov(f.T))
+        v = evecs[:, -len(cls):].flip(1).T.contiguous()
+        z = f @ v.T
+        m, sdv = z.mean(0), z.std(0)
+        print(f"{key}: level {i}: principal std {[round(x, 4) for x in sdv.tolist()]}, feature |mean| "
+              f"{f.abs().mean().item():.3f}", flush=True)
+        w = base[f"model.{det_idx}.cv3.{i}.2.weight"]
+        b = base[f"model.{det_idx}.cv3.{i}.2.bias"]
+        w2, b2 = torch.zeros_like(w), torch.full_like(b, -30.0)
+        w2[cls] = (v * (K / sdv)[:, None]).float()[:, :, None, None]
+        b2[cls] = (-m * K / sdv).float()
+        sd[f"model.{det_idx}.cv3.{i}.2.weight"] = w2
+        sd[f"model.{det_idx}.cv3.{i}.2.bias"] = b2
+        zs.append((cls, (z - m) * K / sdv))
+    # per level: the offset that puts conf midway between the k-th and (k+1)-th largest designed logit of the
+    # median calibration image (k = ceil(target)): about `target` candidates per image on every level
+    lr = level_ranges(s)
+    kk = int(np.ceil(target))
+    lconf = float(np.log(CONF / (1 - CONF)))
+    for i, (cls, zl) in enumerate(zs):
+        na = lr[i][1] - lr[i][0]
+        zmax = zl.reshape(xc.shape[0], na, len(cls)).amax(2)
+        top = torch.sort(zmax, dim=1, descending=True).values
+        cut = float(torch.median((top[:, kk - 1] + top[:, kk]) / 2))
+        off = lconf - cut
+        cnt = (zmax + off > lconf).sum(1).tolist()
+        bkey = f"model.{det_idx}.cv3.{i}.2.bias"
+        sd[bkey] = sd[bkey].clone()
+        sd[bkey][cls] += off
+        print(f"{key}: level {i} offset {off:.3f} (calibration candidates {cnt})", flush=True)
+    model.load_state_dict(sd)
+    model.fuse(verbose=False)
+    return model, sd, det_idx, nl
+
+
+def main():
+    torch.set_num_threads(8)
+    tasks = make_golden.import_reference()
+    make_golden._load_pkg()
+    from ultralytics.utils.nms import non_max_suppression
+
+    E.MIN_CAND = 3
+    keys = sys.argv[1:] or list(CASES)
+    path = HERE / "e2e_nms_ml.npz"
+    out = dict(np.load(path)) if path.exists() else {}
+    for key in keys:
+        t0 = time.time()
+        model, sd, det_idx, nl = build(tasks, key)
+        _, _, bs, s, seed0, gain, _ = CASES[key]
+        per_fwd = 4 if s <= 640 else 2
+        seeds, tries = [], 0
+        for bi in range(bs):
+            sx, t = _search(model, s, seed0 + bi * SEEDS_PER_IMAGE, bi, per_fwd)
+            assert sx is not None, f"{key}: image {bi}: no margin-satisfying input in {SEEDS_PER_IMAGE} seeds"
+            seeds.append(sx)
+            tries += t
+        x = torch.cat([image(sx, s) for sx in seeds])
+        with torch.inference_mode():
+            y = model(x)[0]
+        ok, st = E.margins(y.numpy())
+        assert ok and _levels_ok(y.numpy(), s), st
+        dets, keep = non_max_suppression(y.clone(), CONF, IOU, max_det=MAX_DET, return_idxs=True)
+        for k in [k for k in out if k.startswith(key + "/")]:
+            del out[k]
+        out[f"{key}/seeds"] = np.array(seeds, np.int64)
+        out[f"{key}/gain"] = np.array(gain)
+        out[f"{key}/score_margin"] = np.array(E.SCORE_MARGIN)
+        for i in range(nl):
+            out[f"{key}/cls_w{i}"] = sd[f"model.{det_idx}.cv3.{i}.2.weight"].numpy()
+            out[f"{key}/cls_b{i}"] = sd[f"model.{det_idx}.cv3.{i}.2.bias"].numpy()
+        yn = y.numpy()
+        for b in range(bs):
+            cand = np.nonzero(yn[b, 4:].max(0) > CONF)[0].astype(np.int64)
+            out[f"{key}/keep{b}"] = keep[b].numpy().astype(np.int64)
+            out[f"{key}/det{b}"] = dets[b].numpy()
+            out[f"{key}/cand{b}"] = cand
+            out[f"{key}/y_cand{b}"] = yn[b, :4 + NCLS, cand].T.copy()
+        lv = [[int(((yn[b, 4:].max(0) > CONF)[a0:a1]).sum()) for a0, a1 in level_ranges(s)] for b in range(bs)]
+        print(f"{key}: {tries} forwards, candidates per level {lv}, kept {[int(k.numel()) for k in keep]}, "
+              f"suppressing pairs {sum(v_['suppressing_pairs'] for v_ in st)}, {time.time() - t0:.1f}s", flush=True)
+        np.savez_compressed(path, **out)
+
+
+if __name__ == "__main__":
+    main()

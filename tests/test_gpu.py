@@ -252,14 +252,27 @@ def test_full_size_op_parity(key, full_fx, device):
     assert err <= OP_TOL and e_slice <= OP_TOL and e_sum <= OP_TOL, (err, e_slice, e_sum)
 
 
+def test_fused_c3k2_unknown_tile_is_an_error(device, monkeypatch):
+    """FCE_C3K2_TILE names one of the two instantiated tiles; anything else fails loudly instead of running the
+    tile chosen by map width."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    x = torch.rand(1, 3, 160, 160, generator=torch.Generator().manual_seed(9)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_C3K2", "1")
+    monkeypatch.setenv("FCE_C3K2_TILE", "2,16,8")
+    with pytest.raises(RuntimeError, match="FCE_C3K2_TILE"):
+        eng = Engine(model, 1, 160, device)
+        eng(x)
+        torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("cfg,batch,imgsz,tile", [
     ("yolo11n-fce.yaml", 2, 320, None), ("yolo11s-bifpn.yaml", 2, 256, None), ("yolo11n-fce.yaml", 1, 640, None),
     ("yolo11n-fce.yaml", 1, 224, None), ("yolo11n-fce.yaml", 1, 224, "8,16,4"), ("yolo11n-fce.yaml", 1, 224, "4,40,8"),
-    ("yolo11n-fce.yaml", 1, 224, "2,16,8"), ("yolo11n-fce.yaml", 2, 160, "8,32,4")])
+    ("yolo11n-fce.yaml", 2, 160, "4,40,8")])
 def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device, monkeypatch):
     """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give, whole-graph
-    and per-module; every tile shape the planner picks (8 x 16 on 160^2 maps, 4 x 40 below), forced shapes
-    (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40).  FCE_FUSE_C3K2=1 forces the fused
+    and per-module; every tile shape the planner picks (8 x 16 on 160^2 maps, 4 x 40 below), both tiles forced
+    on every block (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40).  FCE_FUSE_C3K2=1 forces the fused
     form, =0 records the convs only; the default records both and the plan keeps the faster (auto), and every
     combination of forms the auto plan can pick is bitwise the same forward."""
     if tile:
@@ -529,10 +542,12 @@ def test_nms_clustered_suppression_chains(seed, device, nms_path):
 
 @pytest.mark.parametrize("max_nms,max_det", [(1500, 300), (3000, 300), (30000, 3000), (30000, 40)])
 def test_nms_sorted_prefix_select(max_nms, max_det, device, nms_path):
-    """2049..8192 candidates: the first 2048 of the order (score desc, position asc) selected by a radix select
-    over score bits << 13 | (8191 - position) and sorted alone; the full sort when the greedy runs out of the
-    prefix (max_det 3000; heavy suppression with max_det 40) or max_nms truncates inside it (1500).  Most
-    scores tied, the tied group straddling the 2048-th position.  Bit-exact vs the oracle."""
+    """2049..8192 candidates: the first 2048 of the order (score desc, position asc) are selected and sorted
+    alone -- a radix select over the score bits gives the 2048-th score T, every candidate above T is taken and
+    of those scoring exactly T the first `need` in position order (a ballot scan over the candidates' chunk /
+    wave order) -- with the full sort when the greedy runs out of the prefix (max_det 3000; heavy suppression
+    with max_det 40) or max_nms truncates inside it (1500).  Most scores tied, the tied group straddling the
+    2048-th position.  Bit-exact vs the oracle."""
     rng = np.random.default_rng(21)
     B, A, nc = 2, 7000, 5
     p = np.zeros((B, 4 + nc, A), np.float32)
@@ -547,6 +562,29 @@ def test_nms_sorted_prefix_select(max_nms, max_det, device, nms_path):
     pt = torch.from_numpy(p).to(device)
     dets, keep = non_max_suppression(pt, 0.25, 0.7, max_det, max_nms=max_nms, return_idxs=True)
     od, ok = nms_oracle.non_max_suppression(p, 0.25, 0.7, max_det=max_det, max_nms=max_nms)
+    for b in range(B):
+        assert np.array_equal(keep[b].cpu().numpy(), ok[b]), b
+        assert np.array_equal(dets[b].cpu().numpy(), od[b]), b
+
+
+@pytest.mark.parametrize("n1", [0, 1, 2048, 2049, 5000])
+def test_nms_empty_and_small_images_beside_a_large_one(n1, device, nms_path):
+    """Images with no candidate, one, exactly 2048 (the sorted-head capacity) and just past it, in one batch with a
+    5000-candidate image: the empty image takes no select / sort path at all (an empty set once ran the 2048-prefix
+    radix select over stale LDS), and every image is bit-exact vs the oracle."""
+    rng = np.random.default_rng(5)
+    B, A, nc = 3, 6000, 4
+    p = np.zeros((B, 4 + nc, A), np.float32)
+    for b, n in enumerate((0, n1, 5000)):
+        p[b, 0:2] = rng.random((2, A)) * 600
+        p[b, 2:4] = rng.random((2, A)) * 30 + 4
+        idx = rng.permutation(A)[:n]
+        p[b, 4 + rng.integers(0, nc, n), idx] = np.where(rng.random(n) < 0.5, np.float32(0.75),
+                                                         0.3 + 0.6 * rng.random(n)).astype(np.float32)
+    pt = torch.from_numpy(p).to(device)
+    dets, keep = non_max_suppression(pt, 0.25, 0.7, 300, return_idxs=True)
+    od, ok = nms_oracle.non_max_suppression(p, 0.25, 0.7, max_det=300)
+    assert len(ok[0]) == 0 and keep[0].numel() == 0
     for b in range(B):
         assert np.array_equal(keep[b].cpu().numpy(), ok[b]), b
         assert np.array_equal(dets[b].cpu().numpy(), od[b]), b
@@ -748,6 +786,63 @@ def test_end_to_end_nms_indices_640_in_the_shipped_modes(key, e2e_nms640_fx, dev
     for e in sp.pipe.engs:
         e.graph = True
     slots = [sp.submit(xd) for _ in range(5)]
+    for i in range(len(slots) - sp.pipe.depth, len(slots)):
+        check(f"sharded slot {i}", *sp.results(slots[i]))
+    sp.close()
+
+
+@pytest.mark.parametrize("key", list(cases.E2E_NMS_ML))
+def test_end_to_end_nms_indices_all_levels_and_scales(key, e2e_nms_ml_fx, device):
+    """Kept anchor indices bit-equal to the reference's with designed candidates on ALL THREE Detect levels of every
+    image (P3 / P4 / P5 outputs of the HIP forward all reach the NMS), at the n (640, batch 8), l (640, batch 2: the
+    scale of the 8-GPU l256 config's per-rank shard) and m-h8 (1280, batch 2: config 4) scales
+    (make_golden_e2e_nms_ml.py).  Through one executor (graph replay and direct launches, NMS with and without the
+    epilogue's best-class keys), engine.Pipeline with three lanes replaying captured hipGraphs, and
+    dist.ShardedPredictor; scores within the fixture's margin and boxes within BOX_TOL at every candidate anchor."""
+    from fce_yolo_amd.dist import ShardedPredictor
+
+    fx = e2e_nms_ml_fx.group(key)
+    model, x = cases.designed_model_ml(key, fx)
+    _, _, B, S = cases.E2E_NMS_ML[key]
+    model = model.to(device)
+    xd = x.half().to(device)
+
+    def check(tag, dets, keep):
+        for b in range(B):
+            k, d, r = keep[b].cpu().numpy(), dets[b].cpu().numpy(), fx[f"det{b}"]
+            assert np.array_equal(k, fx[f"keep{b}"]), (tag, b, k, fx[f"keep{b}"])
+            assert np.array_equal(d[:, 5], r[:, 5]), (tag, b)
+            assert np.abs(d[:, :4] - r[:, :4]).max() <= BOX_TOL * np.abs(r[:, :4]).max(), (tag, b)
+            assert np.abs(d[:, 4] - r[:, 4]).max() <= float(fx["score_margin"]), (tag, b)
+
+    eng = Engine(model, B, S, device)
+    for graph in (True, False):
+        best = eng.new_best()
+        pred = eng(xd, out=torch.empty_like(eng.pred), best=best, graph=graph)
+        torch.cuda.synchronize()
+        yc = [pred[b, :fx[f"y_cand{b}"].shape[1], torch.from_numpy(fx[f"cand{b}"]).to(device)].cpu().numpy().T
+              for b in range(B)]
+        es = max(np.abs(yc[b][:, 4:] - fx[f"y_cand{b}"][:, 4:]).max() for b in range(B))
+        eb = max(np.abs(yc[b][:, :4] - fx[f"y_cand{b}"][:, :4]).max() / np.abs(fx[f"y_cand{b}"][:, :4]).max()
+                 for b in range(B))
+        print(f"{key} graph={graph}: candidate score err {es:.2e}, box rel {eb:.2e}, kept "
+              f"{[len(fx[f'keep{b}']) for b in range(B)]}")
+        assert es <= CLS_TOL and eb <= BOX_TOL, (es, eb)
+        for use_best in (False, True):
+            nms = NMS(B, eng.anchors, eng.nc, device)
+            nms(pred, best if use_best else None)
+            check(f"engine graph={graph} best={use_best}", *nms.results())
+    pipe = Pipeline(eng, depth=3, lanes=3)
+    for e in pipe.engs:
+        e.graph = True
+    slots = [pipe.submit(x.half().to(device)) for _ in range(4)]  # fresh inputs, dropped right after submit
+    for i in range(len(slots) - pipe.depth, len(slots)):
+        check(f"pipeline slot {i}", *pipe.results(slots[i]))
+    eng.close()
+    sp = ShardedPredictor(model, B, S, device, lanes=3)
+    for e in sp.pipe.engs:
+        e.graph = True
+    slots = [sp.submit(xd) for _ in range(4)]
     for i in range(len(slots) - sp.pipe.depth, len(slots)):
         check(f"sharded slot {i}", *sp.results(slots[i]))
     sp.close()
