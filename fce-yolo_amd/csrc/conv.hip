@@ -725,8 +725,17 @@ static int blocks_per_cu(K kernel, size_t lds) {
   }
   return std::max(1, n);
 }
+// FCE_PERSIST_OCC=k (experiment): at most k resident blocks per CU for the persistent grids, leaving the rest of
+// each CU to the other lanes' kernels
+static int persist_cap(int occ) {
+  static const int cap = [] {
+    const char* e = getenv("FCE_PERSIST_OCC");
+    return e ? atoi(e) : 0;
+  }();
+  return cap > 0 ? std::min(occ, cap) : occ;
+}
 static int ring_slots(int units, int gy, int occ) {
-  return std::max(1, std::min((units + 7) / 8, cus_per_xcd() * occ / std::max(1, gy)));
+  return std::max(1, std::min((units + 7) / 8, cus_per_xcd() * persist_cap(occ) / std::max(1, gy)));
 }
 
 static int ring_nsc(int nsteps) { return nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 6 ? 6 : nsteps <= 8 ? 8 : 0; }

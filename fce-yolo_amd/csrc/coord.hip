@@ -42,6 +42,8 @@ static bool band_pool_ok(int C, int W) { return C >= 256 && C % 64 == 0 && W <= 
 // Rows per pooling band: fixed.  The column means add the bands' partial sums, so the band height sets the
 // summation order; a height chosen by batch size (8 rows below 512 blocks, as before) made an image's pooled
 // columns depend on its batch whenever the fp32 sums were inexact (test_batch_invariance, m-h8 1280 bs16).
+// (Round 5: 32-row bands halve the fp32 partials the column pass reads back, but l32 / m16 BiCoord calls took
+// 254.8 / 419.3 us against 249.7 / 415.3 us with 16: half the blocks.)
 static int band_rows(int, int, int) { return 16; }
 
 static size_t ws_layout(const fce_coord_desc& d, int n, int h, int w, CoordWs* out, float* base) {

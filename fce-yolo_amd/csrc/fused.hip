@@ -371,6 +371,13 @@ static int c3_launch(const C3k2Args& a0, int H, int W, int N, hipStream_t s) {
   }
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, NW * 64, G::LDS) != hipSuccess || occ < 1) occ = 1;
+  {
+    static const int cap = [] {  // FCE_C3K2_OCC=k (experiment): at most k resident blocks per CU
+      const char* e = getenv("FCE_C3K2_OCC");
+      return e ? atoi(e) : 0;
+    }();
+    if (cap > 0) occ = std::min(occ, cap);
+  }
   const int grid = int(std::min<int64_t>(a.ntiles, int64_t(cus) * occ));
   FCE_LAUNCH(k, dim3(unsigned(grid)), dim3(NW * 64), G::LDS, s, a);
   return launch_status("c3k2_fused_kernel");

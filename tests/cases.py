@@ -209,11 +209,12 @@ E2E_NMS640 = {
 
 
 E2E_NMS_ML = {
-    # fixture key: (cfg, -h8 BiCoordCrossAtt heads, batch, imgsz) -- make_golden_e2e_nms_ml.CASES: designed classes on
-    # all three Detect levels; l-fce 640 (the per-rank shard scale of the 8-GPU l256 config), m-fce-h8 1280 (config 4)
+    # fixture key: (cfg, -h8 BiCoordCrossAtt heads, batch, imgsz) -- make_golden_e2e_nms_ml.CASES: n with designed
+    # classes on all three Detect levels; l-fce 640 (the per-rank shard scale of the 8-GPU l256 config) and m-fce-h8
+    # 1280 (config 4) on the P3 and P4 levels
     "yolo11n-fce_640_b8_3lvl": ("yolo11n-fce.yaml", False, 8, 640),
-    "yolo11l-fce_640_b2_3lvl": ("yolo11l-fce.yaml", False, 2, 640),
-    "yolo11m-fce-h8_1280_b2_3lvl": ("yolo11m-fce.yaml", True, 2, 1280),
+    "yolo11l-fce_640_b2": ("yolo11l-fce.yaml", False, 2, 640),
+    "yolo11m-fce-h8_1280_b2": ("yolo11m-fce.yaml", True, 2, 1280),
 }
 
 

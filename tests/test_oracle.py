@@ -123,6 +123,24 @@ def test_oracle_designed_end_to_end_nms_640_matches_reference(key, e2e_nms640_fx
         assert np.abs(dets[b] - fx[f"det{b}"]).max() <= 1e-4 * max(1.0, np.abs(fx[f"det{b}"]).max()), b
 
 
+@pytest.mark.parametrize("key", list(cases.E2E_NMS_ML))
+def test_oracle_designed_end_to_end_nms_levels_and_scales_matches_reference(key, e2e_nms_ml_fx):
+    """Several-level margin-designed cases (make_golden_e2e_nms_ml.py: n 640 on all three levels, l 640 and m-h8
+    1280 on P3 / P4): the oracle's fp32 forward + oracle NMS keep exactly the reference's anchors, the candidates'
+    rows and the kept rows to 1e-4."""
+    fx = e2e_nms_ml_fx.group(key)
+    model, x = cases.designed_model_ml(key, fx)
+    y = cases.oracle_model(model, x, torch.float32).numpy()
+    for b in range(x.shape[0]):
+        ref = fx[f"y_cand{b}"]
+        yc = y[b][:ref.shape[1]][:, fx[f"cand{b}"]].T
+        assert np.abs(yc - ref).max() <= 1e-4 * np.abs(ref).max(), b
+    dets, keeps = nms_oracle.non_max_suppression(y)
+    for b in range(x.shape[0]):
+        assert np.array_equal(keeps[b], fx[f"keep{b}"]), b
+        assert np.abs(dets[b] - fx[f"det{b}"]).max() <= 1e-4 * max(1.0, np.abs(fx[f"det{b}"]).max()), b
+
+
 def _cfg(name):
     """The built-in graph data of the product package (restated from the reference YAMLs)."""
     from fce_yolo_amd.parser import load_cfg
