@@ -54,16 +54,16 @@ def launch_command(argv, env):
 
 
 def default_lanes(model: str, env, gpus: int = 1) -> int:
-    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n and s scales on one GPU
-    (n32 29.3-29.6k vs 28.7-28.8k images/s with 3, s32 16.0-16.1k vs 15.8k, profiles/r03w_*, r03ak_*) and, since
-    round 4's faster kernels, the l scale (l32 5.64-5.65k vs 5.57-5.58k, profiles/r04aq_*); 3 otherwise: the m scale,
-    whose four arenas overflow the MALL (m16-h8 1.83k vs 1.76k images/s with 4, profiles/r04aq_*), and every run with a
-    process group, where RCCL's streams share the hardware queues (one-rank RCCL path 27.8k with 3 lanes x 4 queues,
-    24.8-25.3k with 4 x 8, profiles/r03ad_*)."""
+    """Batches in flight per GPU when --lanes is not given: FCE_LANES, else 4 for the n and s scales (n32 29.3-29.6k
+    vs 28.7-28.8k images/s with 3, s32 16.0-16.1k vs 15.8k, profiles/r03w_*) and, since round 4's faster kernels, the
+    l scale (l32 5.64-5.65k vs 5.57-5.58k, profiles/r04aq_*); 3 on the m scale, whose four arenas overflow the MALL
+    (m16-h8 1.83k vs 1.76k images/s with 4).  The same with or without a process group since round 5: the per-batch
+    all-gather used to cost a four-lane step 17 % (a side-stream wait per batch on the device, 29.7-30.1k against
+    36.0-36.4k, whatever the collective), so multi-GPU runs kept 3 lanes x 4 queues; the host-ordered poster with one
+    collective per `lanes` batches (engine.Poster, dist.ShardedPredictor) measures 36.4-36.7k against 36.4-37.4k
+    without a group (profiles/r05w_*)."""
     if env.get("FCE_LANES"):
         return int(env["FCE_LANES"])
-    if gpus > 1 or int(env.get("WORLD_SIZE", "1") or 1) > 1 or env.get("FCE_DIST_FORCE") == "1":
-        return 3
     stem = Path(model).stem
     scale = stem[6:7] if stem.startswith("yolo11") else ""
     return 4 if scale in ("n", "s", "l") else 3
@@ -411,7 +411,7 @@ def main():
         return
     # this rank's contiguous shard of a global batch of B * world images (dist.ShardedPredictor)
     sp = ShardedPredictor(model, B * world, S, dev, batch_size=B, depth=int(os.environ.get("FCE_PIPE_DEPTH", "2")),
-                          lanes=a.lanes, gather=use_dist)
+                          lanes=a.lanes, gather=use_dist and os.environ.get("FCE_DIST_NO_GATHER") != "1")
     eng = sp.engine
     for e in sp.pipe.engs:
         e.graph = bool(a.graph)

@@ -20,6 +20,7 @@ Images never cross GPUs; the gather is the only per-step collective and the benc
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -138,6 +139,22 @@ class DeviceGather:
         send = torch.zeros(self.nb, dtype=torch.uint8, device=device) if self.batch < self.bmax else None
         return send, torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
 
+    def issue_block(self, src: torch.Tensor, gathered: torch.Tensor):
+        """All-gather a contiguous block of m slots' outputs (m * nb bytes, each slot already in the bmax layout)
+        into gathered[: world * m * nb] ([rank][slot] order) on the current stream: one collective."""
+        dst = gathered[: self.world * src.numel()]
+        if self.nccl or src.device.type == "cpu":
+            dist.all_gather_into_tensor(dst, src)
+        else:
+            out = torch.empty(dst.numel(), dtype=torch.uint8)
+            dist.all_gather_into_tensor(out, src.cpu())
+            dst.copy_(out)
+
+    def unpack_block(self, gathered: torch.Tensor, m: int, j: int):
+        """Slot j of an m-slot block gathered by issue_block -> per-image (dets, keep) in the unsharded order."""
+        blocks = gathered[: self.world * m * self.nb].view(self.world, m, self.nb)[:, j]
+        return unpack_gathered(blocks.reshape(-1), self.sizes, self.max_det)
+
     def issue(self, nms, send, gathered):
         """Gather slot `nms`'s outputs into `gathered` on the current stream."""
         from .engine import NMS
@@ -189,16 +206,20 @@ class ShardedPredictor:
         self.engine = Engine(model, self.batch, imgsz, device)
         self.max_det = nms_kw.get("max_det", 300)
         lanes = max(1, int(lanes))
-        depth = -(-max(depth, lanes) // lanes) * lanes  # Pipeline's slot count
-        # each rank's packed outputs padded to bmax images, so every rank contributes the same bytes
+        # every rank's NMS outputs are laid out for bmax images (the remainder shards' rows padded), and with lanes
+        # one all-gather covers `lanes` consecutive batches (the Pipeline's post groups: one contiguous block)
         self.gather = DeviceGather(self.sizes, self.rank, self.max_det) if self.do_gather else None
-        bufs = [self.gather.buffers(device) for _ in range(depth)] if self.do_gather else []
-        self.send = [b[0] for b in bufs]
-        self.gathered = [b[1] for b in bufs]
-        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.do_gather else None, lanes=lanes, **nms_kw)
+        G = lanes if (self.do_gather and lanes > 1) else 1
+        self.pipe = Pipeline(self.engine, depth, post=self._gather if self.do_gather else None, lanes=lanes,
+                             post_every=G, layout_batch=self.bmax, **nms_kw)
+        self.G = self.pipe.G
+        # one gathered buffer per group of slots (world x G slots)
+        self.gathered = ([torch.zeros(self.world * self.G * self.pipe.nb, dtype=torch.uint8, device=device)
+                          for _ in range(self.pipe.depth // self.G)] if self.do_gather else [])
 
-    def _gather(self, k: int):
-        self.gather.issue(self.pipe.nms[k], self.send[k], self.gathered[k])
+    def _gather(self, k0: int, m: int):
+        nb = self.pipe.nb
+        self.gather.issue_block(self.pipe.outbuf[k0 * nb:(k0 + m) * nb], self.gathered[k0 // self.G])
 
     def submit(self, x: torch.Tensor) -> int:
         if x.shape[0] != self.batch:
@@ -214,13 +235,19 @@ class ShardedPredictor:
         rank's shard only)."""
         if k == self.pipe.pending:
             self.pipe.flush()
+        self.pipe._posted[k].wait()
         self.pipe.nms_done[k].synchronize()
         if self.do_gather:
-            return self.gather.unpack(self.gathered[k])
-        # no collective: this rank's own images only (its shard, in order)
-        return unpack_gathered(self.pipe.nms[k].buf, [self.batch], self.max_det)
+            k0, m = self.pipe.group_of(k)
+            return self.gather.unpack_block(self.gathered[k0 // self.G], m, k - k0)
+        # no collective: this rank's own images only (its shard, in order; the slot laid out for bmax images)
+        nms = self.pipe.nms[k]
+        cnt = nms.counts.tolist()
+        return [nms.dets[i, : cnt[i]] for i in range(self.batch)], [nms.keep[i, : cnt[i]] for i in range(self.batch)]
 
     def close(self):
+        self.pipe.flush()
+        self.pipe.close()
         torch.cuda.synchronize(self.engine.device)
         for e in self.pipe.engs:
             e.close()
@@ -274,7 +301,8 @@ class ShardedHostPredictor:
             raise ValueError(f"empty shard(s) {self.sizes} of a {total}-image batch over {self.world} ranks")
         self.bmax = max(self.sizes)
         self.max_det = max_det
-        self.device_gather = predictor is None and self.do_gather
+        # FCE_HOST_GATHER=1: the per-image host gather for the real predictor too (A/B diagnostics)
+        self.device_gather = predictor is None and self.do_gather and os.environ.get("FCE_HOST_GATHER") != "1"
         if predictor is None:
             from .predict import Predictor
 

@@ -11,7 +11,10 @@ max_nms 30000, max_wh 7680) and returns the same per-image (k, 6) tensors and ke
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
+import queue
+import threading
 
 import torch
 
@@ -153,8 +156,11 @@ class NMS:
     """Device NMS with persistent workspace/outputs (graph-capturable)."""
 
     def __init__(self, batch, anchors, nc, device, conf=0.25, iou=0.7, max_det=300, max_nms=30000, max_wh=7680,
-                 classes=None, agnostic=False, multi_label=False):
-        """`classes` / `agnostic` / `multi_label`: the non-default arguments of nms.py:13-29 (fce_nms_ex)."""
+                 classes=None, agnostic=False, multi_label=False, buf=None, layout_batch=None):
+        """`classes` / `agnostic` / `multi_label`: the non-default arguments of nms.py:13-29 (fce_nms_ex).
+        `buf` / `layout_batch`: the outputs go into the caller's packed buffer (packed_bytes(layout_batch)), laid out
+        for `layout_batch` >= batch images, the first `batch` rows written (a multi-GPU gather sends a remainder
+        shard in the largest shard's layout, and consecutive slots' buffers form one contiguous send block)."""
         self.batch, self.anchors, self.nc = batch, anchors, nc
         self.conf, self.iou, self.max_det, self.max_nms, self.max_wh = conf, iou, max_det, max_nms, max_wh
         self.opts = None
@@ -170,8 +176,15 @@ class NMS:
             nb = N.lib().fce_nms_workspace_bytes(batch, anchors, max_nms)
         self.ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
         # outputs packed in one buffer (keep | dets | counts), so a multi-GPU gather is one collective
-        self.buf = torch.zeros(self.packed_bytes(batch, max_det), dtype=torch.uint8, device=device)
-        self.keep, self.dets, self.counts = self.unpack(self.buf, batch, max_det)
+        lb = batch if layout_batch is None else int(layout_batch)
+        assert lb >= batch
+        nbp = self.packed_bytes(lb, max_det)
+        if buf is None:
+            buf = torch.zeros(nbp, dtype=torch.uint8, device=device)
+        assert buf.dtype == torch.uint8 and buf.numel() == nbp and buf.is_contiguous()
+        self.buf = buf
+        keep, dets, counts = self.unpack(self.buf, lb, max_det)
+        self.keep, self.dets, self.counts = keep[:batch], dets[:batch], counts[:batch]
         self.device = device
 
     @staticmethod
@@ -230,6 +243,63 @@ def non_max_suppression(pred: torch.Tensor, conf_thres=0.25, iou_thres=0.7, max_
     return (dets, keep) if return_idxs else dets
 
 
+class Poster:
+    """Post-processing of finished batches on a side stream, issued from a host thread in submission order.
+
+    `submit(ready, fn, posted)`: once the GPU has passed `ready` (a host wait in the poster's thread), `fn()` runs
+    with the poster's stream current and `posted` is set.  No GPU-side cross-stream wait is enqueued: with four
+    lanes saturating the GPU, one barrier packet per batch on a side queue waiting for a lane's event cost 17 % of
+    the pipelined n32 rate, whatever the side stream then did (a one-rank RCCL group: 29.9-30.1k images/s with a
+    no-op post against 36.0-36.4k without one, profiles/r05s_*; more hardware queues made it worse, 25k at 10-24).
+    Collectives issued here keep the submission order on every rank."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.q: queue.Queue = queue.Queue()
+        self.err = None
+        self.thread = threading.Thread(target=self._run, name="fce-poster", daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        torch.cuda.set_device(self.device)
+        while True:
+            item = self.q.get()
+            if item is None:
+                self.q.task_done()
+                return
+            ready, fn, posted = item
+            try:
+                if self.err is None:
+                    ready.synchronize()
+                    with torch.cuda.stream(self.stream):
+                        fn()
+            except BaseException as e:  # surfaced by the next submit / drain
+                self.err = e
+            finally:
+                posted.set()
+                self.q.task_done()
+
+    def _check(self):
+        if self.err is not None:
+            raise RuntimeError(f"post-processing failed: {self.err!r}") from self.err
+
+    def submit(self, ready: torch.cuda.Event, fn, posted: threading.Event):
+        self._check()
+        posted.clear()
+        self.q.put((ready, fn, posted))
+
+    def drain(self):
+        """Every submitted item has been issued (its GPU work enqueued, not necessarily finished)."""
+        self.q.join()
+        self._check()
+
+    def close(self):
+        if self.thread.is_alive():
+            self.q.put(None)
+            self.thread.join()
+
+
 class Pipeline:
     """Batch pipeline: the NMS of batch i overlaps the forward of batch i+1.
 
@@ -256,11 +326,19 @@ class Pipeline:
     side stream in submission order (collectives stay ordered across ranks).
     """
 
-    def __init__(self, engine: Engine, depth: int = 2, post=None, defer: bool = True, lanes: int = 1, **nms_kw):
-        """`post(k)`, if given, runs on the side stream right after slot k's NMS (e.g. the multi-GPU gather
-        of its outputs, dist.ShardedPredictor); the slot is reused only after it too has finished."""
+    def __init__(self, engine: Engine, depth: int = 2, post=None, defer: bool = True, lanes: int = 1,
+                 post_every: int = 1, layout_batch: int | None = None, **nms_kw):
+        """`post(k0, m)`, if given, runs on a side stream after the NMS of slots k0 .. k0 + m - 1 (e.g. the multi-GPU
+        gather of their outputs, dist.ShardedPredictor); those slots' NMS outputs are reused only after it too has
+        finished.  `post_every` = G (lanes only): one post per G consecutive batches, whose NMS outputs are then one
+        contiguous block (`outbuf[k0 * nb : (k0 + m) * nb]`, nb = NMS.packed_bytes(layout_batch)), so a gather is one
+        collective per G batches; `flush()` posts a partial group.  `layout_batch`: NMS outputs laid out for that
+        many images (the largest shard of a sharded batch)."""
         self.lanes = max(1, int(lanes))
-        depth = -(-max(depth, self.lanes) // self.lanes) * self.lanes  # a multiple of lanes
+        self.G = max(1, int(post_every)) if (post is not None and self.lanes > 1) else 1
+        unit = self.lanes * self.G // math.gcd(self.lanes, self.G)
+        depth = max(depth, self.lanes, 2 * self.G if self.G > 1 else 1)
+        depth = -(-depth // unit) * unit  # a multiple of lanes and of G
         if self.lanes > 1:
             defer = False  # each lane runs its NMS right after its own forward
         self.eng, self.depth, self.post, self.defer = engine, depth, post, defer
@@ -271,7 +349,11 @@ class Pipeline:
         self.lane_done = [torch.cuda.Event() for _ in range(depth)]
         self.preds = [torch.empty_like(engine.pred) for _ in range(depth)]
         self.bests = [engine.new_best() for _ in range(depth)]
-        self.nms = [NMS(engine.batch, engine.anchors, engine.nc, dev, **nms_kw) for _ in range(depth)]
+        lb = engine.batch if layout_batch is None else int(layout_batch)
+        self.nb = NMS.packed_bytes(lb, nms_kw.get("max_det", 300))
+        self.outbuf = torch.zeros(depth * self.nb, dtype=torch.uint8, device=dev)  # slot k: [k nb, (k + 1) nb)
+        self.nms = [NMS(engine.batch, engine.anchors, engine.nc, dev, buf=self.outbuf[k * self.nb:(k + 1) * self.nb],
+                        layout_batch=lb, **nms_kw) for k in range(depth)]
         self.side = torch.cuda.Stream(dev)
         self.fwd_done = [torch.cuda.Event() for _ in range(depth)]
         self.nms_done = [torch.cuda.Event() for _ in range(depth)]
@@ -281,6 +363,18 @@ class Pipeline:
         # diagnostics only (FCE_PIPE_SKIP_NMS=1): lanes run the forwards alone, so the NMS's share of the pipelined
         # step can be measured; the results are then meaningless
         self._skip_nms = os.environ.get("FCE_PIPE_SKIP_NMS") == "1"
+        self._wait_always = os.environ.get("FCE_LANE_WAIT_ALWAYS") == "1"  # diagnostics: the pre-round-5 waits
+        # lanes with post: the posts are issued by a host thread (Poster) once the lanes have finished the group's
+        # batches; FCE_POST_DEVICE_WAIT=1 restores the device-side waits on the side stream (diagnostics)
+        self.poster = None
+        if self.lanes > 1 and post is not None and os.environ.get("FCE_POST_DEVICE_WAIT") != "1":
+            self.poster = Poster(dev)
+            self.side = self.poster.stream
+        self._posted = [threading.Event() for _ in range(depth)]
+        for e in self._posted:
+            e.set()
+        self._group = []  # slots of the current post group not posted yet
+        self._groups = {}  # slot -> (first slot, slots) of the group it was last posted with
         if defer:
             N.call("fce_net_set_fork", engine.net, N.lib().fce_net_fork_hint(engine.net))
 
@@ -291,31 +385,69 @@ class Pipeline:
         with torch.cuda.stream(self.side):
             self.nms[k](self.preds[k], self.bests[k])
             if self.post is not None:
-                self.post(k)
+                self.post(k, 1)
             self.nms_done[k].record(self.side)
+
+    def _post_group(self):
+        """Post the block of G slots the current group's batches went into (consecutive, in submission order).  A
+        partial group (flush) posts the whole block too: its other slots still hold earlier batches whose results are
+        live, and the block's gathered copy is laid out for all G slots."""
+        ks, self._group = self._group, []
+        if not ks:
+            return
+        k0, m = ks[0] - ks[0] % self.G, self.G
+        block = range(k0, k0 + m)
+        done = torch.cuda.Event()
+        for k in block:
+            self.nms_done[k] = done
+            self._groups[k] = (k0, m)
+        if self.poster is not None:
+            ready = [self.lane_done[k] for k in block if self.used[k] or k in ks]
+
+            def fn(k0=k0, m=m, ready=ready, done=done):
+                for e in ready[:-1]:  # the poster waits for every lane's batch of the group on the host
+                    e.synchronize()
+                self.post(k0, m)
+                done.record(self.poster.stream)
+
+            # one poster item per group; the slots' `posted` flags are set together
+            flag = threading.Event()
+            self.poster.submit(ready[-1], fn, flag)
+            for k in block:
+                self._posted[k] = flag
+        else:
+            for k in block:
+                if self.used[k] or k in ks:
+                    self.side.wait_event(self.lane_done[k])
+            with torch.cuda.stream(self.side):
+                self.post(k0, m)
+                done.record(self.side)
 
     def _submit_lane(self, x: torch.Tensor, k: int) -> int:
         lane = k % self.lanes
         s, eng = self.lane_streams[lane], self.engs[lane]
         main = torch.cuda.current_stream(self.eng.device)
         self.in_ready[k].record(main)  # x (and anything the caller queued before) is ready
-        s.wait_event(self.in_ready[k])
-        if self.used[k] and self.post is not None:
-            s.wait_event(self.nms_done[k])  # the side stream's post(k) has read nms[k]
+        if self._wait_always or not self.in_ready[k].query():  # a cross-queue wait is enqueued only when needed
+            s.wait_event(self.in_ready[k])
         x.record_stream(s)  # the lane reads x asynchronously: its block stays allocated until the lane has
         with torch.cuda.stream(s):
             eng(x, out=self.preds[k], best=self.bests[k])
             self.fwd_done[k].record(s)
+            if self.used[k] and self.post is not None:
+                # the post of the slot's previous batch has read nms[k] (pred / best are the lane's own: stream order)
+                self._posted[k].wait()
+                if self._wait_always or not self.nms_done[k].query():
+                    s.wait_event(self.nms_done[k])
             if not self._skip_nms:
                 self.nms[k](self.preds[k], self.bests[k])
             self.lane_done[k].record(s)
         if self.post is None:
             self.nms_done[k] = self.lane_done[k]
         else:
-            self.side.wait_event(self.lane_done[k])
-            with torch.cuda.stream(self.side):
-                self.post(k)
-                self.nms_done[k].record(self.side)
+            self._group.append(k)
+            if len(self._group) == self.G:
+                self._post_group()
         self.used[k] = True
         return k
 
@@ -341,22 +473,38 @@ class Pipeline:
         return k
 
     def flush(self):
-        """Issue the NMS still pending (deferred mode) without waiting for another forward."""
+        """Issue the NMS still pending (deferred mode) without waiting for another forward, the post of a partial
+        group (lanes), and every post still queued on the host: afterwards a device synchronisation covers all
+        submitted work."""
         if self.pending is not None:
             k, self.pending = self.pending, None
             self._issue_nms(k, False)
+        if self._group:
+            self._post_group()
+        if self.poster is not None:
+            self.poster.drain()
+
+    def close(self):
+        if self.poster is not None:
+            self.poster.close()
+
+    def group_of(self, k: int):
+        """(first slot, slots) of the post group slot k was posted with (lanes with post)."""
+        return self._groups.get(k, (k, 1))
 
     def wait(self, k: int | None = None):
         """Make the caller's stream wait for the NMS of slot k (all slots when None)."""
-        if k is None or k == self.pending:
+        if k is None or k == self.pending or (k is not None and k in self._group):
             self.flush()
         main = torch.cuda.current_stream(self.eng.device)
         for j in range(self.depth) if k is None else (k,):
             if self.used[j]:
+                self._posted[j].wait()
                 main.wait_event(self.nms_done[j])
 
     def results(self, k: int):
-        if k == self.pending:
+        if k == self.pending or k in self._group:
             self.flush()
+        self._posted[k].wait()
         self.nms_done[k].synchronize()
         return self.nms[k].results()

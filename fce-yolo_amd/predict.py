@@ -17,12 +17,13 @@ one D2H copy per batch, an executor lane with a captured hipGraph per slot).
 from __future__ import annotations
 
 import ctypes as C
+import threading
 
 import numpy as np
 import torch
 
 from . import _native as N
-from .engine import NMS, Engine
+from .engine import NMS, Engine, Poster
 
 
 class LetterboxImg(C.Structure):  # fce_letterbox_img
@@ -98,6 +99,9 @@ class _Lane:
         self.nms = NMS(batch, eng.anchors, eng.nc, device, **nms_kw)
         self.out_host = torch.empty(self.nms.buf.numel(), dtype=torch.uint8, pin_memory=True)
         self.send = self.gathered = None  # the multi-GPU gather's buffers (Predictor(gather=...))
+        self.chain_done = torch.cuda.Event()  # the lane's chain (gathered path: the poster's host wait)
+        self.posted = threading.Event()
+        self.posted.set()
         self.done = torch.cuda.Event()
         self.ticket = None  # ticket whose results this lane holds (not yet collected)
         self.shapes = []
@@ -184,9 +188,9 @@ class Predictor:
             e.graph = graph
         self.lanes = [_Lane(e, batch, self.device, nms_kw) for e in engs]
         self.gather = gather
-        self.comm = None
+        self.poster = None
         if gather is not None:
-            self.comm = torch.cuda.Stream(self.device)  # the collectives, in batch order
+            self.poster = Poster(self.device)  # the collectives, in batch order, issued from a host thread
             for ln in self.lanes:
                 ln.send, ln.gathered = gather.buffers(self.device)
                 ln.out_host = torch.empty(gather.nbytes, dtype=torch.uint8, pin_memory=True)
@@ -291,15 +295,18 @@ class Predictor:
                    self.max_det, C.c_void_p(sc.data_ptr()), st)
             if self.gather is None:
                 ln.out_host.copy_(ln.nms.buf, non_blocking=True)  # packed keep | dets | counts: one D2H copy
-        if self.gather is not None:  # every rank's packed outputs (side stream, batch order), then one D2H copy
-            self.comm.wait_stream(ln.stream)
-            with torch.cuda.stream(self.comm):
+                ln.done.record(ln.stream)
+            else:
+                ln.chain_done.record(ln.stream)
+        if self.gather is not None:
+            # every rank's packed outputs gathered once the lane's chain is done (host-ordered poster: no side-stream
+            # wait on the device), then one D2H copy of the gathered block
+            def fn(ln=ln):
                 self.gather.issue(ln.nms, ln.send, ln.gathered)
-            ln.stream.wait_stream(self.comm)
-            with torch.cuda.stream(ln.stream):
                 ln.out_host.copy_(ln.gathered, non_blocking=True)
-        with torch.cuda.stream(ln.stream):
-            ln.done.record(ln.stream)
+                ln.done.record(self.poster.stream)
+
+            self.poster.submit(ln.chain_done, fn, ln.posted)
         ln.ticket = i + 1
         ln.shapes = shapes
         return ln.ticket
@@ -313,6 +320,7 @@ class Predictor:
         return self._issue(self._stage(images))
 
     def _collect(self, ln: _Lane):
+        ln.posted.wait()
         ln.done.synchronize()
         if self.gather is not None:
             ln.ticket = None
@@ -360,6 +368,9 @@ class Predictor:
                 yield self.result(q.popleft(), return_idxs)
 
     def close(self):
+        if self.poster is not None:
+            self.poster.drain()
+            self.poster.close()
         torch.cuda.synchronize(self.device)
         self.pool.shutdown()
         for ln in self.lanes:

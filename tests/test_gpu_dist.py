@@ -92,3 +92,86 @@ def test_sharded_host_predictor_two_ranks_match_one_predictor():
             for d, k, d1, k1 in zip(ds, ks, wd, wk):
                 assert np.array_equal(k, k1.numpy()), rank
                 assert np.array_equal(d, d1.numpy()), rank
+
+
+def _worker_resident(rank, world, port, q):
+    """dist.ShardedPredictor over gloo with both ranks on cuda:0: grouped all-gathers (lanes 2 -> one collective per
+    two batches, a partial group at flush), remainder shard in the largest shard's layout."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fce_yolo_amd.dist import ShardedPredictor
+
+        torch.cuda.set_device(0)
+        sp = ShardedPredictor(_model(), TOTAL, S, "cuda:0", batch_size=BS, lanes=2, gather=True, conf=0.05)
+        assert sp.G == 2 and sp.bmax == BS
+        xs = _resident_inputs()
+        slots = [sp.submit(x[sp.start:sp.end].half().to("cuda:0")) for x in xs]
+        sp.flush()
+        out = []
+        for k in slots[-sp.pipe.depth:]:
+            ds, ks = sp.results(k)
+            out.append(([d.cpu().numpy() for d in ds], [kk.cpu().numpy() for kk in ks]))
+        q.put((rank, out))
+        sp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _resident_inputs(nb=5):
+    g = torch.Generator().manual_seed(21)
+    return [torch.rand(TOTAL, 3, S, S, generator=g) for _ in range(nb)]
+
+
+def test_sharded_predictor_grouped_gather_two_ranks_match_one_engine():
+    """Every rank gets every image's detections, bit-equal to one executor + NMS over the whole batch of 7."""
+    from fce_yolo_amd.engine import NMS, Engine
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_resident, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    import queue
+    import time
+
+    res, t0 = [], time.time()
+    while len(res) < len(procs):
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead and time.time() - t0 < 100, f"rank exit codes {[p.exitcode for p in procs]}"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda t: t[0])
+    model = _model()
+    xs = _resident_inputs()
+
+    def reference(bounds):
+        """per batch, per image (dets, keep) from one executor per [lo, hi) range of the batch"""
+        out = [([], []) for _ in xs]
+        for lo, hi in bounds:
+            eng = Engine(model, hi - lo, S, "cuda:0")
+            nms = NMS(hi - lo, eng.anchors, eng.nc, "cuda:0", conf=0.05)
+            for j, x in enumerate(xs):
+                dets, keep, counts = nms(eng(x[lo:hi].half().to("cuda:0")).clone())
+                c = counts.tolist()
+                out[j][0].extend(dets[i, :c[i]].cpu().numpy() for i in range(hi - lo))
+                out[j][1].extend(keep[i, :c[i]].cpu().numpy() for i in range(hi - lo))
+            eng.close()
+        return out[-len(res[0][1]):]
+
+    def diff(out, want):
+        return [(j, i) for j, ((ds, ks), (wd, wk)) in enumerate(zip(out, want)) for i, (d, k, d1, k1) in
+                enumerate(zip(ds, ks, wd, wk)) if not (np.array_equal(k, k1) and np.array_equal(d, d1))]
+
+    per_shard = reference([(0, BS), (BS, TOTAL)])  # the shards' own executors: what the gather must deliver
+    assert sum(len(d) for ds, _ in per_shard for d in ds) > 0
+    for rank, out in res:
+        assert len(out) == len(per_shard) and all(len(ds) == TOTAL for ds, _ in out)
+        assert not diff(out, per_shard), (rank, diff(out, per_shard))
+    whole = reference([(0, TOTAL)])  # one executor over all 7 images (batch invariance of the forward)
+    assert not diff(res[0][1], whole), diff(res[0][1], whole)

@@ -252,10 +252,12 @@ def test_bench_gpus_n_launches_ranks_before_torch():
     assert m.default_lanes("yolo11m-fce-h8.yaml", {}) == 3 and m.default_lanes("yolo11s-bifpn.yaml", {}) == 4
     assert m.hw_queues_env(["--model", "yolo11l-fce.yaml"], {}) == "8"
     assert m.hw_queues_env(["--model", "yolo11m-fce-h8.yaml"], {}) is None
-    # with a process group (N > 1, a rank, or the one-rank RCCL rehearsal): 3 lanes, HIP's queues untouched
-    assert m.default_lanes("yolo11n-fce.yaml", {}, 8) == 3 and m.default_lanes("yolo11n-fce.yaml", {"WORLD_SIZE": "8"}) == 3
-    assert m.hw_queues_env(["--gpus", "8"], {}) is None and m.hw_queues_env([], {"WORLD_SIZE": "2"}) is None
-    assert m.hw_queues_env([], {"FCE_DIST_FORCE": "1"}) is None
+    # with a process group (N > 1, a rank, or the one-rank RCCL rehearsal): the same lanes and queues as one GPU
+    # (round 5: the grouped, host-ordered gather no longer costs a four-lane step)
+    assert m.default_lanes("yolo11n-fce.yaml", {}, 8) == 4 and m.default_lanes("yolo11n-fce.yaml", {"WORLD_SIZE": "8"}) == 4
+    assert m.hw_queues_env(["--gpus", "8"], {}) == "8" and m.hw_queues_env([], {"WORLD_SIZE": "2"}) == "8"
+    assert m.hw_queues_env([], {"FCE_DIST_FORCE": "1"}) == "8"
+    assert m.default_lanes("yolo11m-fce-h8.yaml", {}, 8) == 3
 
 
 def test_bench_world_size_mismatch_fails():
