@@ -5,6 +5,7 @@
 #                           (FCE_HOST_GATHER=1, host path) / no process group; 8 hardware queues in all
 #   dist_ab.sh cost TAG     torchrun alone / the group without the per-batch gather (FCE_DIST_NO_GATHER=1) / with it
 #   dist_ab.sh queues TAG   the group with the device-side wait by GPU_MAX_HW_QUEUES (8 .. 24)
+#   dist_ab.sh host TAG     the host-image path with the poster's per-batch gather against no group, 3 rounds
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 MODE=$1
 OUT=gpurun_out/${2:-dist_ab}
@@ -40,6 +41,12 @@ case "$MODE" in
       run group_nogather_$rep FCE_DIST_NO_GATHER=1 FCE_DIST_FORCE=1 $R --master-port $((29800 + i)) bench.py $A || exit $?
       run group_gather_$rep FCE_DIST_FORCE=1 $R --master-port $((29800 + i)) bench.py $A || exit $?
       run plain_$rep X=0 python bench.py $A || exit $?
+    done
+    ;;
+  host)  # the host-image path only: the poster's per-batch device gather / no process group, 3 interleaved rounds
+    for rep in 1 2 3; do
+      run host_poster_$rep FCE_DIST_FORCE=1 $R --master-port $((29800 + i)) bench.py --source host --steps 100 --warmup 10 || exit $?
+      run host_plain_$rep X=0 python bench.py --source host --steps 100 --warmup 10 || exit $?
     done
     ;;
   every)  # diagnostics: the poster issuing the gather only every n-th batch (results meaningless)
