@@ -161,8 +161,9 @@ def parse_args():
     ap.add_argument("--profile-passes", type=int, default=10, help="per-op HIP-event passes averaged")
     ap.add_argument("--predict-lanes", type=int, default=None,
                     help="batches in flight in the host-image legs (default predict.default_lanes: 5 on n / s, 3 on m / l)")
-    ap.add_argument("--predict-steps", type=int, default=30,
-                    help="batches of the host-image predict path timed after the main line (0 = skip)")
+    ap.add_argument("--predict-steps", type=int, default=100,
+                    help="batches of the host-image predict path timed after the main line (0 = skip; 100: the "
+                         "lanes' fill and drain are a few % of the window, 30 read ~25 %% low, profiles/r05aa_*)")
     ap.add_argument("--dist-config-steps", type=int, default=None,
                     help="N=1 only: also time this many steps in a child rank under the configuration `--gpus N` runs "
                          "(a one-rank RCCL process group, its lanes and hardware queues, the per-batch all-gather) -> "

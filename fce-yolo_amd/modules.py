@@ -174,6 +174,30 @@ def emit_conv(be, conv: nn.Conv2d, bn, act: bool, x: View, out: View | None = No
     return y
 
 
+def conv_native_cat(owner: nn.Module, convs, act: bool, device) -> _ConvNative:
+    """ONE packed 1x1 conv computing several 1x1 stride-1 convs of the same input side by side: their folded weights
+    and biases concatenated along the output channels, in the order given (cached on `owner`, keyed by every conv's
+    and BN's tensors).  Bitwise the separate convs: each output channel sums the same K-steps in the same order
+    whatever the cout tiling, and the epilogue is per channel."""
+    ts = [t for c, bn in convs for t in list(c.parameters()) + list(c.buffers()) +
+          (list(bn.parameters()) + list(bn.buffers()) if bn is not None else [])]
+    key = (str(device), act) + tuple(_tkey(t) for t in ts)
+
+    def build():
+        ws, bs = zip(*(fold_bn(c, bn) for c, bn in convs))
+        w, b = torch.cat(ws), torch.cat(bs)
+        c0 = convs[0][0]
+        desc = N.ConvDesc(c0.in_channels, w.shape[0], 1, 1, 1, N.ACT_SILU if act else N.ACT_NONE, 0, N.EPI_STORE, None,
+                          0, 0)
+        return _ConvNative(desc, pack_conv(desc, w, device), b.to(device).contiguous())
+
+    c = owner.__dict__.get("_fce_cat")
+    if c is None or c[0] != key:
+        c = (key, build())
+        owner.__dict__["_fce_cat"] = c
+    return c[1]
+
+
 def _no_dup() -> bool:
     """C2f / C3k2 bottlenecks read their chunk from the concat record unless FCE_DUP=1 (dense copy from cv1's
     epilogue): measured on n32 the copy takes ~20 us off the 3x3 family and puts ~20 us onto the 1x1 family
@@ -340,8 +364,39 @@ class C3(nn.Module):
         self.cv3 = Conv(2 * c_, c2, 1)
         self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, k=((1, 1), (3, 3)), e=1.0) for _ in range(n)))
 
+    def _cat_ok(self) -> bool:
+        """cv1 and cv2 (both 1x1 s1 over x, block.py:337-339) can run as one conv with concatenated weights
+        (FCE_C3_CAT=0: two convs)."""
+        import os
+
+        if os.environ.get("FCE_C3_CAT", "1") == "0" or not len(self.m):
+            return False
+        c1, c2 = self.cv1.conv, self.cv2.conv
+        return all(c.kernel_size[0] == 1 and c.stride[0] == 1 and c.groups == 1 for c in (c1, c2)) and \
+            self.cv1._act() == self.cv2._act() and c1.out_channels % 8 == 0 and c2.out_channels % 8 == 0
+
     def emit(self, be, x, out=None):
         c_ = self.cv1.conv.out_channels
+        if self._cat_ok():
+            # rec = [m | b | a]: cv3 reads [m | b] (cat(m(cv1(x)), cv2(x)), block.py:340), and b = cv2(x), a = cv1(x)
+            # come from ONE conv over x (x read once, one launch); below 64 channels a dense copy of a is stored too
+            # (the bottlenecks' 3x3 then reads whole lines, as FCE_DUP does for C2f)
+            c2 = self.cv2.conv.out_channels
+            rec = be.alloc(x.n, 2 * c_ + c2, x.h, x.w)
+            y = rec.slice(c_, c2 + c_)
+            a = rec.slice(c_ + c2, c_)
+            if not be.shape_only:
+                nat = conv_native_cat(self, [(self.cv2.conv, getattr(self.cv2, "bn", None)),
+                                             (self.cv1.conv, getattr(self.cv1, "bn", None))], self.cv1._act(), be.device)
+                xin = be.from_torch(x.buf) if (x.layout == N.NCHW and isinstance(be, EagerBackend)) else x
+                if getattr(be, "supports_dup", False) and c_ < 64 and not x.up:
+                    a = be.alloc(x.n, c_, x.h, x.w)
+                    be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None, dup=(a, c2))
+                else:
+                    be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None)
+            for i, m in enumerate(self.m):
+                a = m.emit(be, a, out=rec.slice(0, c_) if i == len(self.m) - 1 else None)
+            return self.cv3.emit(be, rec.slice(0, c_ + c2), out=out)
         buf = be.alloc(x.n, 2 * c_, x.h, x.w)
         a = self.cv1.emit(be, x) if len(self.m) else self.cv1.emit(be, x, out=buf.slice(0, c_))
         for i, m in enumerate(self.m):

@@ -252,6 +252,36 @@ def test_full_size_op_parity(key, full_fx, device):
     assert err <= OP_TOL and e_slice <= OP_TOL and e_sum <= OP_TOL, (err, e_slice, e_sum)
 
 
+@pytest.mark.parametrize("cfg,batch,imgsz", [("yolo11n-fce.yaml", 2, 320), ("yolo11l-fce.yaml", 1, 256),
+                                              ("yolo11m-fce.yaml", 1, 192)])
+def test_c3_concatenated_cv1_cv2_bitwise(cfg, batch, imgsz, device, monkeypatch):
+    """C3 / C3k's cv1 and cv2 (both 1x1 over x) as ONE conv with concatenated weights (modules.C3.emit, the
+    default) give the forward bit for bit what the two convs give (FCE_C3_CAT=0), whole-graph (with the dense copy
+    of the bottlenecks' input below 64 channels) and per module (eager drop-in)."""
+    model = cases.seeded_model(cfg, 0).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(4)).half().to(device)
+    monkeypatch.setenv("FCE_C3_CAT", "0")
+    e0 = Engine(model, batch, imgsz, device)
+    y0 = e0(x).clone()
+    n0 = e0.num_ops()
+    monkeypatch.setenv("FCE_C3_CAT", "1")
+    e1 = Engine(model, batch, imgsz, device)
+    y1 = e1(x).clone()
+    torch.cuda.synchronize()
+    n_c3k = sum(1 for m in model.modules() if isinstance(m, M.C3k))
+    assert n_c3k > 0 and e1.num_ops() == n0 - n_c3k
+    assert torch.equal(y0, y1)
+    c3 = next(m for m in model.modules() if isinstance(m, M.C3k))
+    xi = torch.randn(batch, c3.cv1.conv.in_channels, 24, 20, device=device).half().contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        u1 = c3(xi)
+        monkeypatch.setenv("FCE_C3_CAT", "0")
+        u0 = c3(xi)
+    torch.cuda.synchronize()
+    assert torch.equal(u0, u1)
+
+
 def test_fused_c3k2_unknown_tile_is_an_error(device, monkeypatch):
     """FCE_C3K2_TILE names one of the two instantiated tiles; anything else fails loudly instead of running the
     tile chosen by map width."""
