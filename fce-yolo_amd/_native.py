@@ -92,6 +92,17 @@ class C3k2Desc(C.Structure):
     ]
 
 
+class DclsDesc(C.Structure):
+    """fce_dcls_desc: the Detect cls branch of one level (w / b: dw1, pw1, dw2, pw2, cls)."""
+    _fields_ = [
+        ("c0", C.c_int),
+        ("c3", C.c_int),
+        ("nc", C.c_int),
+        ("w", C.c_void_p * 5),
+        ("b", C.c_void_p * 5),
+    ]
+
+
 class NmsOpts(C.Structure):
     """fce_nms_opts: the non-default arguments of non_max_suppression (utils/nms.py:13-29)."""
     _fields_ = [
@@ -114,6 +125,7 @@ _PT = C.POINTER(Tensor)
 _PCD = C.POINTER(ConvDesc)
 _PCO = C.POINTER(CoordDesc)
 _PC3 = C.POINTER(C3k2Desc)
+_PDC = C.POINTER(DclsDesc)
 
 _SIGS = {
     "fce_last_error": (C.c_char_p, []),
@@ -138,6 +150,11 @@ _SIGS = {
     "fce_net_c3k2_form": (_I, [_P, _I]),
     "fce_net_set_c3k2_form": (_I, [_P, _I, _I]),
     "fce_net_op_skipped": (_I, [_P, _I]),
+    "fce_detect_cls_supported": (_I, [_PDC]),
+    "fce_detect_cls": (_I, [_PDC, _PT, C.POINTER(DetectEpi), _P]),
+    "fce_net_add_detect_cls_alt": (_I, [_P, _PDC, _I, _I, _I, _I]),
+    "fce_net_alt_form": (_I, [_P, _I]),
+    "fce_net_set_alt_form": (_I, [_P, _I, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

@@ -285,6 +285,11 @@ class NetBackend:
         autotune keeps the faster form (fce_net_add_c3k2_alt)."""
         N.call("fce_net_add_c3k2_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
 
+    def detect_cls_alt(self, desc: N.DclsDesc, x: View, first_op: int, nops: int):
+        """The one-kernel Detect cls branch as the alternative of ops [first_op, first_op + nops) (its two depthwise and
+        two 1x1 convs and its cls tail): the plan-time autotune keeps the faster form (fce_net_add_detect_cls_alt)."""
+        N.call("fce_net_add_detect_cls_alt", self.net, C.byref(desc), x.buf, x.coff, first_op, nops)
+
     def psa(self, qkv: View, heads: int, kd: int, hd: int, pe_w: int, pe_b: int, y: View):
         assert qkv.coff == 0 and qkv.c == qkv.cstride
         N.call("fce_net_add_psa_attention", self.net, qkv.buf, heads, kd, hd, pe_w, pe_b, y.buf, y.coff)

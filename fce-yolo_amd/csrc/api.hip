@@ -45,6 +45,8 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
 
 bool c3k2_fused_ok(const fce_c3k2_desc& d);
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
+bool detect_cls_fused_ok(const fce_dcls_desc& d);
+int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_detect_epi& e, hipStream_t s);
 
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
 int scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* sc, hipStream_t s);
@@ -122,6 +124,11 @@ int fce_c3k2_supported(const fce_c3k2_desc* d) { return d && c3k2_fused_ok(*d) ?
 int fce_c3k2(const fce_c3k2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
   FCE_CHECK(d && x && y, "fce_c3k2: null argument");
   FCE_GUARD(return c3k2_fused(*d, *x, *y, S(stream));)
+}
+int fce_detect_cls_supported(const fce_dcls_desc* d) { return d && detect_cls_fused_ok(*d) ? 1 : 0; }
+int fce_detect_cls(const fce_dcls_desc* d, const fce_tensor* x, const fce_detect_epi* e, void* stream) {
+  FCE_CHECK(d && x && e, "fce_detect_cls: null argument");
+  FCE_GUARD(return detect_cls_fused(*d, *x, *e, S(stream));)
 }
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
                       const fce_detect_epi* e, void* stream) {
@@ -207,7 +214,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2 };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -234,12 +241,14 @@ struct OpDesc {
   int box[4] = {0, 0, 0, 0}, cls[4] = {0, 0, 0, 0};
   float strides[4] = {0, 0, 0, 0};
   int reg_max = 16;
-  int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT
+  int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT, OP_DCLS (part 1)
   fce_c3k2_desc c3k2{};              // OP_C3K2
+  fce_dcls_desc dcls{};              // OP_DCLS
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
   int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
-  // alternative forms: an OP_C3K2 added by fce_net_add_c3k2_alt computes the same output as ops [alt_first,
-  // alt_first + alt_n) (its four convs); exactly one form runs, the other's ops are skipped (plan-time choice)
+  // alternative forms: an OP_C3K2 / OP_DCLS added by fce_net_add_c3k2_alt / fce_net_add_detect_cls_alt computes the
+  // same output as ops [alt_first, alt_first + alt_n) (its four convs / its five ops); exactly one form runs, the
+  // other's ops are skipped (plan-time choice)
   int alt_first = -1, alt_n = 0;
   bool skip = false;
 };
@@ -400,6 +409,11 @@ int run_op_impl(fce_net* net, const OpDesc& op, const fce_tensor& input, float* 
                        net->cur_best};
       return conv2d_detect(op.conv, x, op.w, op.b, e, s, op.tile);
     }
+    case OP_DCLS: {
+      fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, 1, op.strides[0],
+                       net->cur_best};
+      return detect_cls_fused(op.dcls, x, e, s);
+    }
     case OP_DETECT: {
       fce_tensor bx[4], cl[4];
       for (int i = 0; i < op.nl; ++i) {
@@ -472,6 +486,11 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
       a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
       a.push_back({kBufPred, 2 * op.level + op.part, 2 * op.level + op.part + 1, true});
       a.push_back({kBufBest, op.level, op.level + 1, true});  // box zeroes, cls maxes: keep them ordered
+      break;
+    case OP_DCLS:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.dcls.c0, false});
+      a.push_back({kBufPred, 2 * op.level + 1, 2 * op.level + 2, true});
+      a.push_back({kBufBest, op.level, op.level + 1, true});
       break;
     case OP_DETECT:
       for (int i = 0; i < op.nl; ++i) a.push_back({op.box[i], 0, net->bufs[op.box[i]].c, false});
@@ -594,6 +613,20 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       *flops = 2.0 * N * (3.0 * op.coord.mid * op.coord.inp * L + op.coord.oup * op.coord.mid * L);
       break;
     }
+    case OP_DCLS: {  // one read of x, one write of the fp32 scores, the five ops' weights
+      const fce_dcls_desc& d = op.dcls;
+      *name = "detect_cls_fused";
+      const double px = N * hw(op.in);
+      const fce_conv_desc cs[5] = {{d.c0, d.c0, 3, 1, d.c0, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c0, d.c3, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c3, d.c3, 3, 1, d.c3, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c3, d.c3, 1, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0},
+                                   {d.c3, d.nc, 1, 1, 1, FCE_ACT_NONE, 0, FCE_EPI_STORE, nullptr, 0, 0}};
+      *bytes = px * d.c0 * 2 + px * d.nc * 4;
+      for (const fce_conv_desc& c : cs) *bytes += double(conv_weight_bytes(c));
+      *flops = 2.0 * px * (9.0 * d.c0 + double(d.c0) * d.c3 + 9.0 * d.c3 + double(d.c3) * d.c3 + double(d.c3) * d.nc);
+      break;
+    }
     case OP_C3K2: {  // one read of x, one write of y, the four convs' weights
       const fce_c3k2_desc& d = op.c3k2;
       *name = "c3k2_fused";
@@ -624,8 +657,8 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
   }
 }
 
-// the active form of an alternative: the fused op, or the convs it replaces
-void set_c3k2_form(fce_net* net, OpDesc& op, bool fused) {
+// the active form of an alternative: the fused op, or the ops it replaces
+void set_alt_form(fce_net* net, OpDesc& op, bool fused) {
   if (op.skip != !fused) net->drop_graph();  // captured forwards hold the other form's launches
   op.skip = !fused;
   for (int j = op.alt_first; j < op.alt_first + op.alt_n; ++j) net->ops[j].skip = fused;
@@ -809,7 +842,7 @@ int fce_net_add_c3k2_alt(fce_net* net, const fce_c3k2_desc* d, int in, int in_co
   OpDesc& op = net->ops.back();
   op.alt_first = first_op;
   op.alt_n = nops;
-  set_c3k2_form(net, op, true);  // fused until the plan-time autotune says otherwise
+  set_alt_form(net, op, true);  // fused until the plan-time autotune says otherwise
   return FCE_OK;
 }
 
@@ -821,7 +854,63 @@ int fce_net_c3k2_form(const fce_net* net, int i) {
 
 int fce_net_set_c3k2_form(fce_net* net, int i, int fused) {
   FCE_CHECK(fce_net_c3k2_form(net, i) >= 0, "fce_net_set_c3k2_form: not a fused C3k2 op with an alternative");
-  set_c3k2_form(net, net->ops[i], fused != 0);
+  set_alt_form(net, net->ops[i], fused != 0);
+  return FCE_OK;
+}
+
+int fce_net_alt_form(const fce_net* net, int i) {
+  if (!net || i < 0 || i >= int(net->ops.size())) return -1;
+  const OpDesc& op = net->ops[i];
+  return op.alt_first >= 0 ? (op.skip ? 0 : 1) : -1;
+}
+
+int fce_net_set_alt_form(fce_net* net, int i, int fused) {
+  FCE_CHECK(fce_net_alt_form(net, i) >= 0, "fce_net_set_alt_form: not a fused op with an alternative");
+  set_alt_form(net, net->ops[i], fused != 0);
+  return FCE_OK;
+}
+
+int fce_net_add_detect_cls_alt(fce_net* net, const fce_dcls_desc* d, int in, int in_coff, int first_op, int nops) {
+  FCE_CHECK(net && d && valid_buf(net, in, false) && nops == 5 && first_op >= 0 &&
+                first_op + nops == int(net->ops.size()),
+            "fce_net_add_detect_cls_alt: the alternative must be the last five ops added");
+  FCE_CHECK(detect_cls_fused_ok(*d), "fce_net_add_detect_cls_alt: unsupported channel configuration");
+  const OpDesc* o = &net->ops[first_op];
+  for (int j = 0; j < 5; ++j)
+    FCE_CHECK(!o[j].skip && o[j].alt_first < 0 && o[j].kind == (j < 4 ? OP_CONV : OP_CONV_DETECT),
+              "fce_net_add_detect_cls_alt: the alternative must be four conv ops and a conv-detect op");
+  const int ks[5] = {3, 1, 3, 1, 1}, cin[5] = {d->c0, d->c0, d->c3, d->c3, d->c3};
+  const int cout[5] = {d->c0, d->c3, d->c3, d->c3, d->nc};
+  for (int j = 0; j < 5; ++j) {
+    const fce_conv_desc& c = o[j].conv;
+    FCE_CHECK(c.k == ks[j] && c.cin == cin[j] && c.cout == cout[j] && c.stride == 1 && c.up == 0 &&
+                  c.groups == (ks[j] == 3 ? c.cin : 1) && c.act == (j < 4 ? FCE_ACT_SILU : FCE_ACT_NONE) &&
+                  c.epilogue == FCE_EPI_STORE && o[j].w == d->w[j] && o[j].b == d->b[j],
+              "fce_net_add_detect_cls_alt: the five ops are not this branch (shapes, activations or weights differ)");
+  }
+  // the chain: x -> dw1 -> pw1 -> dw2 -> pw2 -> cls, each reading the previous op's whole output
+  FCE_CHECK(o[0].in == in && o[0].in_coff == in_coff && o[0].res < 0 && o[0].dup < 0,
+            "fce_net_add_detect_cls_alt: the first op must read the given input");
+  for (int j = 1; j < 5; ++j)
+    FCE_CHECK(o[j].in == o[j - 1].out && o[j].in_coff == o[j - 1].out_coff && o[j].res < 0 && o[j].dup < 0,
+              "fce_net_add_detect_cls_alt: the five ops must form one chain");
+  FCE_CHECK(o[4].part == 1 && o[4].nc == d->nc, "fce_net_add_detect_cls_alt: the last op must be the cls tail");
+  OpDesc op;
+  op.kind = OP_DCLS;
+  op.dcls = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->c0;
+  op.level = o[4].level;
+  op.strides[0] = o[4].strides[0];
+  op.nc = o[4].nc;
+  op.reg_max = o[4].reg_max;
+  op.part = 1;
+  op.alt_first = first_op;
+  op.alt_n = nops;
+  net->drop_graph();
+  net->ops.push_back(op);
+  set_alt_form(net, net->ops.back(), true);  // fused until the plan-time autotune says otherwise
   return FCE_OK;
 }
 
@@ -946,13 +1035,17 @@ static int autotune(fce_net* net) {
     op.tile = best;
     if (st) break;
   }
-  // alternative forms (fused C3k2 against its four tuned convs): time both on the planned shapes, keep the faster
-  // (FCE_FUSE_C3K2=1 keeps the fused form without timing).  Logged as codes 0xF01 (fused) / 0xF00 (the convs).
-  const char* fe = getenv("FCE_FUSE_C3K2");
-  const bool force_fused = fe && strcmp(fe, "1") == 0;
-  for (size_t i = 0; i < net->ops.size() && st == FCE_OK && !force_fused; ++i) {
+  // alternative forms (fused C3k2 against its four tuned convs, fused Detect cls branch against its five tuned ops):
+  // time both on the planned shapes, keep the faster (FCE_FUSE_C3K2=1 / FCE_FUSE_DCLS=1 keep the fused form without
+  // timing).  Logged as codes 0xF01 (fused) / 0xF00 (the unfused ops).
+  auto forced = [](const char* name) {
+    const char* e = getenv(name);
+    return e && strcmp(e, "1") == 0;
+  };
+  const bool force_c3k2 = forced("FCE_FUSE_C3K2"), force_dcls = forced("FCE_FUSE_DCLS");
+  for (size_t i = 0; i < net->ops.size() && st == FCE_OK; ++i) {
     OpDesc& op = net->ops[i];
-    if (op.kind != OP_C3K2 || op.alt_first < 0) continue;
+    if (op.alt_first < 0 || (op.kind == OP_C3K2 && force_c3k2) || (op.kind == OP_DCLS && force_dcls)) continue;
     float t[2] = {1e30f, 1e30f};  // [convs, fused]
     for (int form = 0; form < 2 && st == FCE_OK; ++form) {
       auto run_form = [&]() {
@@ -975,7 +1068,7 @@ static int autotune(fce_net* net) {
       }
       if (st == FCE_OK) net->tune_log.push_back({int(i), 0xF00 | form, t[form]});
     }
-    if (st == FCE_OK) set_c3k2_form(net, op, t[1] <= t[0]);
+    if (st == FCE_OK) set_alt_form(net, op, t[1] <= t[0]);
   }
   if (hipStreamSynchronize(ts) != hipSuccess && st == FCE_OK) st = fail(FCE_ERR_HIP, "fce_net_plan: autotune failed");
   cleanup();

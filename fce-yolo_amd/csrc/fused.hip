@@ -28,7 +28,7 @@
 // fpin before every fp16 conversion).
 #include <algorithm>
 
-#include "common.h"
+#include "mfma_stage.h"
 
 namespace fce {
 
@@ -68,52 +68,12 @@ struct C3k2Args {
   int diag;           // FCE_C3K2_DIAG: block 0 prints its per-stage clocks
 };
 
-// Barrier between the stages of one tile: the LDS writes published (lgkmcnt(0)), the global traffic left in flight
-// (__syncthreads() also waits vmcnt(0), i.e. for the next tile's x prefetch at the barrier after stage 1 and for
-// the tile's y stores at its end; measured the same either way, round 5, the kernel's time being its stage chain)
-__device__ __forceinline__ void c3_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ h4 c3_h4(const float (&v)[4]) {
-  return h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])};
-}
-
 // SiLU(acc + bias) of lane group grp's 4 couts of tile ct (the bias from the block's LDS copy: a global load in
 // an epilogue would make it wait for the next tile's x prefetch, vmcnt retiring in issue order)
 __device__ __forceinline__ void c3_act(const float* bias, int ct, int grp, const f4& acc, float (&v)[4]) {
   const int co0 = ct * 16 + grp * 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = silu(acc[j] + bias[co0 + j]);
-}
-
-// One stage for the wave's MF fragments (fragment f = wave + NW i) x CT cout tiles over NS K-steps, fully
-// unrolled: A from the stage's LDS fragments ([ct][step][lane]), B = bl(i, step); then epi(i, ct, acc).
-template <int MF, int CT, int NS, typename BL, typename EPI>
-__device__ __forceinline__ void c3_stage(const h8* wl, BL bl, EPI epi) {
-  f4 acc[MF][CT];
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[i][ct] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int st = 0; st < NS; ++st) {
-    h8 av[CT], bv[MF];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) av[ct] = wl[(ct * NS + st) * 64];
-#pragma unroll
-    for (int i = 0; i < MF; ++i) bv[i] = bl(i, st);
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[ct], bv[i], acc[i][ct], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) epi(i, ct, acc[i][ct]);
 }
 
 // (tap, 8-channel chunk, real step) of K-step st for lane group grp: chunk-major steps (cin % 32 == 0) are
@@ -176,21 +136,7 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
     float* bias = reinterpret_cast<float*>(sm + G::OB);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int nfr = cts[s] * nss[s] * 64;
-      for (int e0 = int(threadIdx.x); e0 < nfr; e0 += 4 * NW * 64) {
-        h8 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = e0 + u * NW * 64;
-          const int k = e >> 6, ct = k / nss[s], stp = k - ct * nss[s];
-          if (e < nfr) v[u] = a.w[s][(size_t(ct) * a.nalloc[s] + stp) * 64 + (e & 63)];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = e0 + u * NW * 64;
-          if (e < nfr) sm[wofs[s] + e] = v[u];
-        }
-      }
+      stage_copy_frags(sm + wofs[s], a.w[s], cts[s], nss[s], a.nalloc[s], NW * 64);
       for (int e = int(threadIdx.x); e < cts[s] * 16; e += NW * 64) bias[bofs[s] + e] = e < couts[s] ? a.b[s][e] : 0.f;
     }
   }
@@ -226,16 +172,16 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         const int iy = y0 - 2 + r, ix = x0 - 2 + cq;
         float v[4];
         c3_act(bias, ct, grp, acc, v);
-        h4 o = c3_h4(v);
+        h4 o = h4_of(v);
         if (!(iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)) o = h4{0, 0, 0, 0};  // the 3x3s' zero padding of b
         *reinterpret_cast<h4*>(T + (q * G::sT) * 8 + ct * 16 + grp * 4) = o;
       };
-      c3_stage<G::MF1, G::CT1, G::NS1>(sm + lane, bl, epi);
+      mfma_stage<G::MF1, G::CT1, G::NS1>(sm + lane, bl, epi);
     }
     tick(0);
     if (t + 1 < t_end) load_x(t + 1);  // in flight during stages 2-4
     tick(1);
-    c3_barrier();
+    stage_barrier();
     // ---------------- stage 2: h = m.cv1(b) over the m.cv1 region (3x3 from the t image)
     {
       int pb[G::MF2];
@@ -259,14 +205,14 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         const int iy = y0 - 1 + r, ix = x0 - 1 + cq;
         float v[4];
         c3_act(bias + G::B2, ct, grp, acc, v);
-        h4 o = c3_h4(v);
+        h4 o = h4_of(v);
         if (!(iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)) o = h4{0, 0, 0, 0};
         *reinterpret_cast<h4*>(Hh + (q * G::sH) * 8 + ct * 16 + grp * 4) = o;
       };
-      c3_stage<G::MF2, G::CT2, G::NS2>(sm + G::OW2 + lane, bl, epi);
+      mfma_stage<G::MF2, G::CT2, G::NS2>(sm + G::OW2 + lane, bl, epi);
     }
     tick(2);
-    c3_barrier();
+    stage_barrier();
     // ---------------- stage 3: m = m.cv2(h) + b over the tile (3x3 from the h image)
     {
       int pb[G::MF4];
@@ -293,12 +239,12 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         const h4 rv = *reinterpret_cast<const h4*>(T + (((r + 2) * G::R2W + cq + 2) * G::sT) * 8 + C + co0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
-        *reinterpret_cast<h4*>(Mm + (q * G::sM) * 8 + co0) = c3_h4(v);
+        *reinterpret_cast<h4*>(Mm + (q * G::sM) * 8 + co0) = h4_of(v);
       };
-      c3_stage<G::MF4, G::CT3, G::NS3>(sm + G::OW3 + lane, bl, epi);
+      mfma_stage<G::MF4, G::CT3, G::NS3>(sm + G::OW3 + lane, bl, epi);
     }
     tick(3);
-    c3_barrier();
+    stage_barrier();
     // ---------------- stage 4: y = cv2([a | b | m]) over the tile, to HBM
     {
       int pt[G::MF4], pm[G::MF4];
@@ -322,12 +268,12 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         if (iy >= a.H || ix >= a.W) return;
         float v[4];
         c3_act(bias + G::B4, ct, grp, acc, v);
-        *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + ct * 16 + grp * 4) = c3_h4(v);
+        *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + ct * 16 + grp * 4) = h4_of(v);
       };
-      c3_stage<G::MF4, G::CT4, G::NS4>(sm + G::OW4 + lane, bl, epi);
+      mfma_stage<G::MF4, G::CT4, G::NS4>(sm + G::OW4 + lane, bl, epi);
     }
     tick(4);
-    c3_barrier();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
+    stage_barrier();  // stage 4's reads of t / m before the next tile's stage 1 overwrites them
     tick(5);
   }
   if (a.diag && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -407,11 +353,6 @@ static int c3_inst(const fce_c3k2_desc& d) {
 
 bool c3k2_fused_ok(const fce_c3k2_desc& d) { return c3_inst(d) >= 0; }
 
-static int c3_nalloc(int cin, int k) {  // dense_geom's per-cout-tile fragment count
-  const int nsteps = (k * k * (cin / 8) + 3) / 4;
-  return ((nsteps + 7) & ~7) + 8;
-}
-
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s) {
   const int inst = c3_inst(d);
   FCE_CHECK(inst >= 0, "c3k2 fused: unsupported channel configuration");
@@ -432,7 +373,7 @@ int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y,
   for (int i = 0; i < 4; ++i) {
     a.w[i] = static_cast<const h8*>(d.w[i]);
     a.b[i] = d.b[i];
-    a.nalloc[i] = c3_nalloc(cins[i], ks[i]);
+    a.nalloc[i] = stage_nalloc(cins[i], ks[i]);
   }
   {
     const char* de = getenv("FCE_C3K2_DIAG");

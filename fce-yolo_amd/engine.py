@@ -97,10 +97,18 @@ class Engine:
         for i in range(self.num_ops()):
             if self.variants(i):
                 e.set_variant(i, self.variant(i))
-            f = self.c3k2_form(i)
+            f = self.alt_form(i)
             if f >= 0:
-                e.set_c3k2_form(i, bool(f))
+                e.set_alt_form(i, bool(f))
         return e
+
+    def alt_form(self, i: int) -> int:
+        """1: op i (a fused C3k2 or Detect cls branch with the ops it replaces as the alternative) runs fused; 0: the
+        ops run; -1: other op."""
+        return N.lib().fce_net_alt_form(self.be.net, i)
+
+    def set_alt_form(self, i: int, fused: bool) -> None:
+        N.call("fce_net_set_alt_form", self.be.net, i, int(bool(fused)))
 
     def c3k2_form(self, i: int) -> int:
         """1: op i (a fused C3k2 with its four convs as the alternative) runs fused; 0: the convs run; -1: other op."""

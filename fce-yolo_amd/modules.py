@@ -854,19 +854,63 @@ class Detect(nn.Module):
             pred = torch.empty((xs[0].n, 4 + self.nc, A), dtype=torch.float32, device=be.device)
         off = 0
         for i, x in enumerate(xs):
+            if fused_only:
+                self._emit_level(be, x, i, strides[i])
+                continue
             feats = self._branches(be, x, i)
-            if not fused_only:
-                maps.append(self._raw_map(be, feats, i))
+            maps.append(self._raw_map(be, feats, i))
             for (part, conv), v in zip(self._finals(i), feats):
                 nat = conv_native(conv, None, False, be.device)
-                if fused_only:
-                    be.conv_detect(nat.desc, v, part, i, strides[i], self.nc, self.reg_max, nat.w.data_ptr(),
-                                   nat.b.data_ptr())
-                else:
-                    be.conv_detect(nat.desc, v, pred, A, off, part, strides[i], self.nc, self.reg_max,
-                                   nat.w.data_ptr(), nat.b.data_ptr())
+                be.conv_detect(nat.desc, v, pred, A, off, part, strides[i], self.nc, self.reg_max,
+                               nat.w.data_ptr(), nat.b.data_ptr())
             off += x.h * x.w
         return pred, maps
+
+    def _tail(self, be, part, conv, v, i, stride):
+        nat = conv_native(conv, None, False, be.device)
+        be.conv_detect(nat.desc, v, part, i, stride, self.nc, self.reg_max, nat.w.data_ptr(), nat.b.data_ptr())
+
+    def _emit_level(self, be, x, i, stride):
+        """Graph backend, level i: the box branch and its DFL tail, then the cls branch and its sigmoid tail (the box
+        tail zeroes the level's best-class keys that the cls tail maxes into).  Where csrc/detect_cls.hip has the
+        level's (c0, c3, nc), the cls branch's five ops get the one-kernel form as their alternative
+        (fce_net_add_detect_cls_alt; FCE_FUSE_DCLS: unset / "auto" -- the plan keeps the faster, "1" -- the fused
+        kernel, "0" -- the five ops only)."""
+        self._tail(be, 0, self.cv2[i][2], self.cv2[i][1].emit(be, self.cv2[i][0].emit(be, x)), i, stride)
+        d = self._dcls_desc(be, x, i)
+        first = be.num_ops() if d is not None else 0
+        seq = self.cv3[i]
+        if self.legacy:
+            c = seq[1].emit(be, seq[0].emit(be, x))
+        else:
+            c = seq[0][1].emit(be, seq[0][0].emit(be, x))
+            c = seq[1][1].emit(be, seq[1][0].emit(be, c))
+        self._tail(be, 1, seq[2], c, i, stride)
+        if d is not None and be.num_ops() - first == 5:
+            be.detect_cls_alt(d, x, first, 5)
+
+    def _dcls_desc(self, be, x, i):
+        """fce_dcls_desc of level i's cls branch, or None where the one-kernel form does not apply."""
+        import os
+
+        if os.environ.get("FCE_FUSE_DCLS", "auto") == "0" or self.legacy or not hasattr(be, "detect_cls_alt"):
+            return None
+        if x.up or x.layout != N.NHWC or x.dtype != N.F16:
+            return None
+        seq = self.cv3[i]
+        convs = (seq[0][0], seq[0][1], seq[1][0], seq[1][1])
+        for cv, k in zip(convs, (3, 1, 3, 1)):
+            c = cv.conv
+            if c.kernel_size[0] != k or c.stride[0] != 1 or not isinstance(cv.act, nn.SiLU):
+                return None
+        d = N.DclsDesc()
+        d.c0, d.c3, d.nc = x.c, seq[0][1].conv.out_channels, self.nc
+        for j, cv in enumerate(convs):
+            nat = conv_native(cv.conv, getattr(cv, "bn", None), True, be.device)
+            d.w[j], d.b[j] = nat.w.data_ptr(), nat.b.data_ptr()
+        nat = conv_native(seq[2], None, False, be.device)
+        d.w[4], d.b[4] = nat.w.data_ptr(), nat.b.data_ptr()
+        return d if N.lib().fce_detect_cls_supported(C.byref(d)) else None
 
     def forward(self, x):
         xs = list(x)

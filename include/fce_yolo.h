@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 5
+#define FCE_ABI_VERSION 6
 
 /* status codes */
 #define FCE_OK 0
@@ -207,6 +207,20 @@ typedef struct fce_c3k2_desc {
 int fce_c3k2_supported(const fce_c3k2_desc* d);
 int fce_c3k2(const fce_c3k2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
 
+/* Detect cls branch of one level (head.py:86-107, legacy = False: DWConv(c0, c0, 3) -> Conv(c0, c3, 1) ->
+ * DWConv(c3, c3, 3) -> Conv(c3, c3, 1) -> nn.Conv2d(c3, nc, 1), all but the last with SiLU) ending in the cls
+ * epilogue of fce_conv2d_detect (e->part 1: sigmoid into pred rows 4.., the best-class key), in one kernel (t1..t4
+ * stay in LDS).  w / b in the order dw1, pw1, dw2, pw2, cls: the five convs' fce_conv_pack_weights images (the
+ * depthwise ones fp32 [9][c]) and BN-folded biases.  Bitwise equal to the five fce_conv2d / fce_conv2d_detect calls.
+ * fce_detect_cls_supported: the instantiated (c0, c3, nc).  ABI v6. */
+typedef struct fce_dcls_desc {
+  int c0, c3, nc;
+  const void* w[5];
+  const float* b[5];
+} fce_dcls_desc;
+int fce_detect_cls_supported(const fce_dcls_desc* d);
+int fce_detect_cls(const fce_dcls_desc* d, const fce_tensor* x, const fce_detect_epi* e, void* stream);
+
 /* ---------------------------------------------------------------- NMS */
 size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 /* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
@@ -276,6 +290,15 @@ int fce_net_add_c3k2_alt(fce_net* net, const fce_c3k2_desc* d, int in_buf, int i
 /* 1 = op i (an fce_net_add_c3k2_alt op) runs fused, 0 = its convs run, -1 = not such an op */
 int fce_net_c3k2_form(const fce_net* net, int i);
 int fce_net_set_c3k2_form(fce_net* net, int i, int fused);
+/* The fused Detect cls branch (fce_detect_cls) as an ALTERNATIVE to the nops (= 5) ops just added: the branch's two
+ * depthwise and two 1x1 fce_net_add_conv ops and its cls fce_net_add_conv_detect, one chain from (in_buf, in_coff)
+ * with the weights of d.  Exactly one form runs; the plan-time autotune keeps the faster (FCE_FUSE_DCLS=1: the fused
+ * form).  ABI v6. */
+int fce_net_add_detect_cls_alt(fce_net* net, const fce_dcls_desc* d, int in_buf, int in_coff, int first_op, int nops);
+/* Any alternative op (fused C3k2 or fused Detect cls branch): 1 = the fused form runs, 0 = the ops it replaces run,
+ * -1 = op i is not an alternative.  ABI v6. */
+int fce_net_alt_form(const fce_net* net, int i);
+int fce_net_set_alt_form(fce_net* net, int i, int fused);
 /* 1 when op i belongs to the inactive form of an alternative (it launches nothing; profile / op_info report 0) */
 int fce_net_op_skipped(const fce_net* net, int i);
 /* map_bufs[i]: f32 buffer of level i holding cat(box 4*reg_max, cls nc) channels (head.py:122) */

@@ -341,6 +341,119 @@ def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device,
     assert torch.equal(u, f)
 
 
+@pytest.mark.parametrize("batch,imgsz,tiles", [
+    (2, 320, None), (1, 640, None), (1, 224, None), (2, 320, ("8,8,4", "8,8,4")), (1, 224, ("8,16,4", "8,8,4")),
+    (1, 224, ("8,8,4", "8,8,8"))])
+def test_fused_detect_cls_bitwise_equal_to_five_ops(batch, imgsz, tiles, device, monkeypatch):
+    """The one-kernel Detect cls branch (csrc/detect_cls.hip) writes bit for bit the scores and best-class keys its five
+    ops write (dw 3x3, 1x1, dw 3x3, 1x1, cls 1x1 + sigmoid), whole-graph, on both instantiated levels (n P3 / P4),
+    every tile (FCE_DCLS_TILE_64 / _128) and partial edge tiles (224: 28^2 / 14^2 maps).  FCE_FUSE_DCLS=1 forces the
+    fused form, =0 records the five ops only, the default records both and the plan keeps the faster; every
+    combination of forms is bitwise the same forward."""
+    if tiles:
+        monkeypatch.setenv("FCE_DCLS_TILE_64", tiles[0])
+        monkeypatch.setenv("FCE_DCLS_TILE_128", tiles[1])
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(13)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_DCLS", "1")
+    eng = Engine(model, batch, imgsz, device)
+    assert [eng.op_info(i)[0] for i in range(eng.num_ops())].count("detect_cls_fused") == 2
+    yf, bf = eng(x).clone(), eng.best.clone()
+    monkeypatch.setenv("FCE_FUSE_DCLS", "0")
+    eng2 = Engine(model, batch, imgsz, device)
+    assert "detect_cls_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
+    yu, bu = eng2(x).clone(), eng2.best.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(yf, yu) and torch.equal(bf, bu)
+    monkeypatch.delenv("FCE_FUSE_DCLS")
+    ea = Engine(model, batch, imgsz, device)
+    alts = [i for i in range(ea.num_ops()) if ea.alt_form(i) >= 0 and ea.op_info(i)[0] == "detect_cls_fused"]
+    assert len(alts) == 2 and ea.num_ops() == eng2.num_ops() + 2
+    assert torch.equal(ea(x).clone(), yu)
+    for fused in (False, True):
+        for i in alts:
+            ea.set_alt_form(i, fused)
+        assert all(ea.skipped(j) == fused for i in alts for j in range(i - 5, i)) and all(ea.skipped(i) != fused
+                                                                                          for i in alts)
+        assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea.best, bu)
+        assert torch.equal(ea(x, graph=False).clone(), yu)
+
+
+def test_fused_detect_cls_unknown_tile_is_an_error(device, monkeypatch):
+    """FCE_DCLS_TILE_64 / _128 name a tile of that instantiation; anything else fails loudly."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    x = torch.rand(1, 3, 160, 160, generator=torch.Generator().manual_seed(9)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_DCLS", "1")
+    monkeypatch.setenv("FCE_DCLS_TILE_128", "8,16,8")
+    with pytest.raises(RuntimeError, match="FCE_DCLS_TILE_128"):
+        eng = Engine(model, 1, 160, device)
+        eng(x)
+        torch.cuda.synchronize()
+
+
+def test_fused_detect_cls_c_abi_views_and_parity(device):
+    """fce_detect_cls through the C-ABI on a channel-slice input view (64 of 96 channels at offset 16), a 19 x 37
+    map (partial tiles both ways) and a level block inside a wider anchor range: equal to the five fce_conv2d /
+    fce_conv2d_detect calls bit for bit (scores and keys), the other anchors untouched, and within the op tolerance
+    of an fp64 torch restatement of the branch."""
+    n, c0, c3, nc, H, W = 2, 64, 80, 80, 19, 37
+    g = torch.Generator().manual_seed(77)
+    specs = [(c0, c0, 3, c0, N.ACT_SILU), (c0, c3, 1, 1, N.ACT_SILU), (c3, c3, 3, c3, N.ACT_SILU),
+             (c3, c3, 1, 1, N.ACT_SILU), (c3, nc, 1, 1, N.ACT_NONE)]
+    ws, bs, descs, packed = [], [], [], []
+    for cin, cout, k, grp, act in specs:
+        w = torch.randn(cout, cin // grp, k, k, generator=g) * (1.5 / (cin // grp * k * k) ** 0.5)
+        b = torch.randn(cout, generator=g) * 0.2
+        d = N.ConvDesc(cin, cout, k, 1, grp, act, 0, N.EPI_STORE, None, 0, 0)
+        ws.append(w), bs.append(b.float().to(device)), descs.append(d), packed.append(M.pack_conv(d, w, device))
+    xbuf = torch.randn(n, H, W, 96, generator=g).half().to(device)
+    xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, n, c0, H, W, 96, 16)
+    A, a0 = H * W + 50, 20
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def run(fused):
+        pred = torch.full((n, 4 + nc, A), float("nan"), device=device)
+        best = torch.zeros(n, A, dtype=torch.int64, device=device)
+        e = N.DetectEpi(pred.data_ptr(), A, a0, nc, 16, 1, 8.0, best.data_ptr())
+        if fused:
+            d = N.DclsDesc()
+            d.c0, d.c3, d.nc = c0, c3, nc
+            for j in range(5):
+                d.w[j], d.b[j] = packed[j].data_ptr(), bs[j].data_ptr()
+            N.call("fce_detect_cls", C.byref(d), C.byref(xt), C.byref(e), stream)
+        else:
+            cur = xt
+            keep = []
+            for j in range(4):
+                y = torch.empty(n, H, W, specs[j][1], dtype=torch.float16, device=device)
+                keep.append(y)
+                yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, n, specs[j][1], H, W, specs[j][1], 0)
+                N.call("fce_conv2d", C.byref(descs[j]), C.byref(cur), packed[j].data_ptr(), bs[j].data_ptr(), None,
+                       C.byref(yt), stream)
+                cur = yt
+            N.call("fce_conv2d_detect", C.byref(descs[4]), C.byref(cur), packed[4].data_ptr(), bs[4].data_ptr(),
+                   C.byref(e), stream)
+        torch.cuda.synchronize()
+        return pred.cpu(), best.cpu()
+
+    pf, bf = run(True)
+    pu, bu = run(False)
+    assert torch.equal(pf[:, 4:, a0:a0 + H * W], pu[:, 4:, a0:a0 + H * W]) and torch.equal(bf, bu)
+    assert torch.isnan(pf[:, :4]).all() and torch.isnan(pf[:, 4:, :a0]).all() and torch.isnan(pf[:, 4:, a0 + H * W:]).all()
+    assert (bf[:, :a0] == 0).all() and (bf[:, a0 + H * W:] == 0).all() and (bf[:, a0:a0 + H * W] != 0).all()
+    t = xbuf[..., 16:16 + c0].permute(0, 3, 1, 2).double().cpu()
+    F = torch.nn.functional
+    for j, (cin, cout, k, grp, act) in enumerate(specs):
+        t = F.conv2d(t, ws[j].double(), bs[j].double().cpu(), padding=k // 2, groups=grp)
+        t = F.silu(t) if act == N.ACT_SILU else torch.sigmoid(t)
+        if j < 4:
+            t = t.half().double()  # the unfused ops store fp16 intermediates
+    ref = t.reshape(n, nc, H * W)
+    err = (pf[:, 4:, a0:a0 + H * W].double() - ref).abs().max().item()
+    print(f"OPERR detect_cls {err:.3e}")
+    assert err <= 2e-3, err
+
+
 @pytest.mark.parametrize("cfg,mut,batch,imgsz", [("yolo11n-fce.yaml", None, 2, 320), ("yolo11s-bifpn.yaml", None, 2, 256)])
 def test_c2f_dense_chunk_copy_bitwise(cfg, mut, batch, imgsz, device, monkeypatch):
     """With FCE_DUP=1 whole-graph lowering stores the chunk a C2f / C3k2's first block reads densely from cv1's

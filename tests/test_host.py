@@ -92,7 +92,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(L, s)]
     assert not missing, missing
     assert declared <= set(N.EXPORTED) | {"fce_net_create", "fce_net_destroy"}
-    assert L.fce_abi_version() == 5
+    assert L.fce_abi_version() == 6
 
 
 def test_device_count_without_gpu_is_safe():
