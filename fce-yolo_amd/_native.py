@@ -103,6 +103,16 @@ class DclsDesc(C.Structure):
     ]
 
 
+class Stem2Desc(C.Structure):
+    """fce_stem2_desc: the backbone's first two convs (w / b: stem, second conv)."""
+    _fields_ = [
+        ("c0", C.c_int),
+        ("c1", C.c_int),
+        ("w", C.c_void_p * 2),
+        ("b", C.c_void_p * 2),
+    ]
+
+
 class NmsOpts(C.Structure):
     """fce_nms_opts: the non-default arguments of non_max_suppression (utils/nms.py:13-29)."""
     _fields_ = [
@@ -126,6 +136,7 @@ _PCD = C.POINTER(ConvDesc)
 _PCO = C.POINTER(CoordDesc)
 _PC3 = C.POINTER(C3k2Desc)
 _PDC = C.POINTER(DclsDesc)
+_PST = C.POINTER(Stem2Desc)
 
 _SIGS = {
     "fce_last_error": (C.c_char_p, []),
@@ -154,6 +165,9 @@ _SIGS = {
     "fce_detect_cls": (_I, [_PDC, _PT, C.POINTER(DetectEpi), _P]),
     "fce_net_add_detect_cls_alt": (_I, [_P, _PDC, _I, _I, _I, _I]),
     "fce_net_alt_form": (_I, [_P, _I]),
+    "fce_stem_fused_supported": (_I, [_PST]),
+    "fce_stem_fused": (_I, [_PST, _PT, _PT, _P]),
+    "fce_net_add_stem_alt": (_I, [_P, _PST, _I, _I]),
     "fce_net_set_alt_form": (_I, [_P, _I, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

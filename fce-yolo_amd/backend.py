@@ -285,6 +285,12 @@ class NetBackend:
         autotune keeps the faster form (fce_net_add_c3k2_alt)."""
         N.call("fce_net_add_c3k2_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
 
+    def stem_alt(self, desc: N.Stem2Desc, first_op: int, nops: int):
+        """The one-kernel stem pair as the alternative of ops [first_op, first_op + nops) (the stem and the second conv):
+        the plan keeps the faster form, or the two convs when anything else reads the stem's output
+        (fce_net_add_stem_alt)."""
+        N.call("fce_net_add_stem_alt", self.net, C.byref(desc), first_op, nops)
+
     def detect_cls_alt(self, desc: N.DclsDesc, x: View, first_op: int, nops: int):
         """The one-kernel Detect cls branch as the alternative of ops [first_op, first_op + nops) (its two depthwise and
         two 1x1 convs and its cls tail): the plan-time autotune keeps the faster form (fce_net_add_detect_cls_alt)."""

@@ -46,6 +46,8 @@ int nms(const float* pred, const unsigned long long* best, int n, int nc, int A,
 bool c3k2_fused_ok(const fce_c3k2_desc& d);
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 bool detect_cls_fused_ok(const fce_dcls_desc& d);
+bool stem_fused_ok(const fce_stem2_desc& d);
+int stem_fused(const fce_stem2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_detect_epi& e, hipStream_t s);
 
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
@@ -129,6 +131,11 @@ int fce_detect_cls_supported(const fce_dcls_desc* d) { return d && detect_cls_fu
 int fce_detect_cls(const fce_dcls_desc* d, const fce_tensor* x, const fce_detect_epi* e, void* stream) {
   FCE_CHECK(d && x && e, "fce_detect_cls: null argument");
   FCE_GUARD(return detect_cls_fused(*d, *x, *e, S(stream));)
+}
+int fce_stem_fused_supported(const fce_stem2_desc* d) { return d && stem_fused_ok(*d) ? 1 : 0; }
+int fce_stem_fused(const fce_stem2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
+  FCE_CHECK(d && x && y, "fce_stem_fused: null argument");
+  FCE_GUARD(return stem_fused(*d, *x, *y, S(stream));)
 }
 int fce_conv2d_detect(const fce_conv_desc* d, const fce_tensor* x, const void* w, const float* bias,
                       const fce_detect_epi* e, void* stream) {
@@ -214,7 +221,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS, OP_STEM2 };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -244,12 +251,14 @@ struct OpDesc {
   int part = 0, level = 0, nc = 0;  // OP_CONV_DETECT, OP_DCLS (part 1)
   fce_c3k2_desc c3k2{};              // OP_C3K2
   fce_dcls_desc dcls{};              // OP_DCLS
+  fce_stem2_desc stem2{};            // OP_STEM2
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
   int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
   // alternative forms: an OP_C3K2 / OP_DCLS added by fce_net_add_c3k2_alt / fce_net_add_detect_cls_alt computes the
   // same output as ops [alt_first, alt_first + alt_n) (its four convs / its five ops); exactly one form runs, the
   // other's ops are skipped (plan-time choice)
   int alt_first = -1, alt_n = 0;
+  bool alt_locked = false;  // the alternative cannot run in this net (fce_net_plan found a reason): the ops it replaces run
   bool skip = false;
 };
 
@@ -409,6 +418,10 @@ int run_op_impl(fce_net* net, const OpDesc& op, const fce_tensor& input, float* 
                        net->cur_best};
       return conv2d_detect(op.conv, x, op.w, op.b, e, s, op.tile);
     }
+    case OP_STEM2: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.stem2.c1);
+      return stem_fused(op.stem2, x, y, s);
+    }
     case OP_DCLS: {
       fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, 1, op.strides[0],
                        net->cur_best};
@@ -486,6 +499,9 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
       a.push_back({op.in, op.in_coff, op.in_coff + op.conv.cin, false});
       a.push_back({kBufPred, 2 * op.level + op.part, 2 * op.level + op.part + 1, true});
       a.push_back({kBufBest, op.level, op.level + 1, true});  // box zeroes, cls maxes: keep them ordered
+      break;
+    case OP_STEM2:
+      a.push_back({op.out, op.out_coff, op.out_coff + op.stem2.c1, true});
       break;
     case OP_DCLS:
       a.push_back({op.in, op.in_coff, op.in_coff + op.dcls.c0, false});
@@ -611,6 +627,16 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       *bytes = px * op.coord.inp * 2 * 2 + px * op.coord.oup * 2;  // 2 reads (pool, gate) + 1 write
       const double L = double(net->H >> net->bufs[op.in].shift) + double(net->W >> net->bufs[op.in].shift);
       *flops = 2.0 * N * (3.0 * op.coord.mid * op.coord.inp * L + op.coord.oup * op.coord.mid * L);
+      break;
+    }
+    case OP_STEM2: {  // one read of the f16 input, one write of the second conv's output, both convs' weights
+      const fce_stem2_desc& d = op.stem2;
+      *name = "stem_fused";
+      const double ohw = hw(op.out), ihw = double(net->H) * net->W;
+      const fce_conv_desc c0{3, d.c0, 3, 2, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+      const fce_conv_desc c1{d.c0, d.c1, 3, 2, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+      *bytes = N * ihw * 3 * 2 + N * ohw * d.c1 * 2 + double(conv_weight_bytes(c0)) + double(conv_weight_bytes(c1));
+      *flops = 2.0 * N * (ihw / 4.0 * d.c0 * 27.0 + ohw * d.c1 * 9.0 * d.c0);
       break;
     }
     case OP_DCLS: {  // one read of x, one write of the fp32 scores, the five ops' weights
@@ -866,7 +892,40 @@ int fce_net_alt_form(const fce_net* net, int i) {
 
 int fce_net_set_alt_form(fce_net* net, int i, int fused) {
   FCE_CHECK(fce_net_alt_form(net, i) >= 0, "fce_net_set_alt_form: not a fused op with an alternative");
+  FCE_CHECK(!fused || !net->ops[i].alt_locked, "fce_net_set_alt_form: this fused op cannot run in this net");
   set_alt_form(net, net->ops[i], fused != 0);
+  return FCE_OK;
+}
+
+int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, int nops) {
+  FCE_CHECK(net && d && nops == 2 && first_op >= 0 && first_op + nops == int(net->ops.size()),
+            "fce_net_add_stem_alt: the alternative must be the last two ops added");
+  FCE_CHECK(stem_fused_ok(*d), "fce_net_add_stem_alt: unsupported channel configuration");
+  const OpDesc& s0 = net->ops[first_op];
+  const OpDesc& s1 = net->ops[first_op + 1];
+  const fce_conv_desc &c0 = s0.conv, &c1 = s1.conv;
+  FCE_CHECK(s0.kind == OP_CONV && s1.kind == OP_CONV && !s0.skip && !s1.skip && s0.alt_first < 0 && s1.alt_first < 0,
+            "fce_net_add_stem_alt: the alternative must be two conv ops");
+  FCE_CHECK(s0.in == -1 && c0.cin == 3 && c0.cout == d->c0 && c0.k == 3 && c0.stride == 2 && c0.groups == 1 &&
+                c0.act == FCE_ACT_SILU && c0.epilogue == FCE_EPI_STORE && s0.res < 0 && s0.dup < 0 && s0.w == d->w[0] &&
+                s0.b == d->b[0],
+            "fce_net_add_stem_alt: the first op must be the 3x3 stride-2 SiLU stem on the network input");
+  FCE_CHECK(s1.in == s0.out && s1.in_coff == s0.out_coff && c1.cin == d->c0 && c1.cout == d->c1 && c1.k == 3 &&
+                c1.stride == 2 && c1.groups == 1 && c1.up == 0 && c1.act == FCE_ACT_SILU &&
+                c1.epilogue == FCE_EPI_STORE && s1.res < 0 && s1.dup < 0 && s1.w == d->w[1] && s1.b == d->b[1],
+            "fce_net_add_stem_alt: the second op must be the 3x3 stride-2 SiLU conv of the stem's output");
+  OpDesc op;
+  op.kind = OP_STEM2;
+  op.stem2 = *d;
+  op.in = -1;
+  op.in_c = 3;
+  op.out = s1.out;
+  op.out_coff = s1.out_coff;
+  op.alt_first = first_op;
+  op.alt_n = nops;
+  net->drop_graph();
+  net->ops.push_back(op);
+  set_alt_form(net, net->ops.back(), true);  // fused until the plan-time autotune says otherwise
   return FCE_OK;
 }
 
@@ -989,7 +1048,12 @@ static int autotune(fce_net* net) {
   int nc = 0;
   for (const OpDesc& op : net->ops)
     if (op.kind == OP_CONV_DETECT) nc = std::max(nc, op.nc);
+  // a dummy network input (f16 NCHW, zeros) for timing the alternatives that read it (the fused stem pair)
+  void* tin = nullptr;
+  bool need_in = false;
+  for (const OpDesc& op : net->ops) need_in |= op.kind == OP_STEM2 && op.alt_first >= 0 && !op.alt_locked;
   auto cleanup = [&]() {
+    if (tin) (void)hipFree(tin);
     if (pred) (void)hipFree(pred);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -1003,6 +1067,15 @@ static int autotune(fce_net* net) {
     return fail(FCE_ERR_HIP, "fce_net_plan: autotune setup failed");
   }
   fce_tensor none{};
+  fce_tensor input{};
+  if (need_in) {
+    const size_t nb = size_t(net->batch) * 3 * net->H * net->W * sizeof(_Float16);
+    if (hipMalloc(&tin, nb) != hipSuccess || hipMemset(tin, 0, nb) != hipSuccess) {
+      cleanup();
+      return fail(FCE_ERR_HIP, "fce_net_plan: autotune input allocation failed");
+    }
+    input = fce_tensor{tin, FCE_F16, FCE_NCHW, net->batch, 3, net->H, net->W, 3, 0};
+  }
   for (OpDesc& op : net->ops) {
     if (!(op.kind == OP_CONV && op.in >= 0) && op.kind != OP_CONV_DETECT) continue;
     int cand[128];
@@ -1042,16 +1115,19 @@ static int autotune(fce_net* net) {
     const char* e = getenv(name);
     return e && strcmp(e, "1") == 0;
   };
-  const bool force_c3k2 = forced("FCE_FUSE_C3K2"), force_dcls = forced("FCE_FUSE_DCLS");
+  const bool force_c3k2 = forced("FCE_FUSE_C3K2"), force_dcls = forced("FCE_FUSE_DCLS"),
+             force_stem = forced("FCE_FUSE_STEM");
   for (size_t i = 0; i < net->ops.size() && st == FCE_OK; ++i) {
     OpDesc& op = net->ops[i];
-    if (op.alt_first < 0 || (op.kind == OP_C3K2 && force_c3k2) || (op.kind == OP_DCLS && force_dcls)) continue;
+    if (op.alt_first < 0 || op.alt_locked || (op.kind == OP_C3K2 && force_c3k2) || (op.kind == OP_DCLS && force_dcls) ||
+        (op.kind == OP_STEM2 && force_stem))
+      continue;
     float t[2] = {1e30f, 1e30f};  // [convs, fused]
     for (int form = 0; form < 2 && st == FCE_OK; ++form) {
       auto run_form = [&]() {
-        if (form == 1) return run_op_impl(net, op, none, pred, ts);
+        if (form == 1) return run_op_impl(net, op, input, pred, ts);
         for (int j = op.alt_first; j < op.alt_first + op.alt_n; ++j) {
-          const int r = run_op_impl(net, net->ops[j], none, pred, ts);
+          const int r = run_op_impl(net, net->ops[j], input, pred, ts);
           if (r) return r;
         }
         return FCE_OK;
@@ -1121,6 +1197,22 @@ int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags) {
     }
     net->anchors = A;
     net->ws_bytes = ws;
+    // a fused stem pair skips writing the stem's output: valid only when nothing but the second conv reads it
+    for (size_t i = 0; i < net->ops.size(); ++i) {
+      OpDesc& op = net->ops[i];
+      if (op.kind != OP_STEM2 || op.alt_first < 0 || op.alt_locked) continue;
+      const OpDesc& s0 = net->ops[op.alt_first];
+      std::vector<Access> acc;
+      for (size_t j = 0; j < net->ops.size() && !op.alt_locked; ++j) {
+        if (int(j) == op.alt_first || int(j) == op.alt_first + 1 || j == i) continue;
+        OpDesc probe = net->ops[j];
+        probe.skip = false;
+        op_accesses(net, probe, acc);
+        for (const Access& x : acc)
+          if (x.buf == s0.out && x.c0 < s0.out_coff + s0.conv.cout && s0.out_coff < x.c1) op.alt_locked = true;
+      }
+      if (op.alt_locked) set_alt_form(net, op, false);
+    }
     FCE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&net->arena), std::max<size_t>(off, 256)));
     FCE_HIP_CHECK(hipMalloc(&net->ws, ws));
     FCE_HIP_CHECK(hipMemset(net->arena, 0, std::max<size_t>(off, 256)));

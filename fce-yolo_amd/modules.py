@@ -261,6 +261,32 @@ class Conv(nn.Module):
         return _run_eager(self, x, keep_nchw=self.conv.in_channels <= 4)
 
 
+def stem_alt(be, m0, m1, first: int, saved: bool):
+    """Graph backend, after the backbone's first two layers were emitted as ops [first, first + 2): where they are
+    Conv(3, c0, 3, 2) -> Conv(c0, c1, 3, 2) (SiLU) with an instantiated (c0, c1) and the stem's output read by nothing
+    else (`saved`: a later layer takes it), record the one-kernel form (csrc/stem_fused.hip) as their alternative.
+    FCE_FUSE_STEM: unset / "auto" -- the plan keeps the faster, "1" -- the fused kernel, "0" -- the two convs only."""
+    import os
+
+    if os.environ.get("FCE_FUSE_STEM", "auto") == "0" or saved or not hasattr(be, "stem_alt"):
+        return
+    if type(m0) is not Conv or type(m1) is not Conv or getattr(m1, "f", -1) != -1 or be.num_ops() - first != 2:
+        return
+    c0, c1 = m0.conv, m1.conv
+    if (c0.in_channels, c0.kernel_size[0], c0.stride[0], c0.groups) != (3, 3, 2, 1) or \
+            (c1.in_channels, c1.kernel_size[0], c1.stride[0], c1.groups) != (c0.out_channels, 3, 2, 1):
+        return
+    if not (isinstance(m0.act, nn.SiLU) and isinstance(m1.act, nn.SiLU)):
+        return
+    d = N.Stem2Desc()
+    d.c0, d.c1 = c0.out_channels, c1.out_channels
+    for j, m in enumerate((m0, m1)):
+        nat = conv_native(m.conv, getattr(m, "bn", None), True, be.device)
+        d.w[j], d.b[j] = nat.w.data_ptr(), nat.b.data_ptr()
+    if N.lib().fce_stem_fused_supported(C.byref(d)):
+        be.stem_alt(d, first, 2)
+
+
 class DWConv(Conv):
     """conv.py:185-200."""
 

@@ -196,11 +196,14 @@ class DetectionModel(nn.Module):
     def emit(self, be, x):
         """_predict_once over a backend; returns (pred, maps)."""
         y = []
+        first = be.num_ops() if hasattr(be, "stem_alt") else None
         for m in self.model:
             if m.f != -1:
                 x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
             x = m.emit(be, x)
             y.append(x if m.i in self.save else None)
+            if m.i == 1 and first is not None:  # the stem pair's one-kernel alternative (modules.stem_alt)
+                M.stem_alt(be, self.model[0], self.model[1], first, 0 in self.save)
         return x
 
     def forward(self, x):

@@ -221,6 +221,18 @@ typedef struct fce_dcls_desc {
 int fce_detect_cls_supported(const fce_dcls_desc* d);
 int fce_detect_cls(const fce_dcls_desc* d, const fce_tensor* x, const fce_detect_epi* e, void* stream);
 
+/* The backbone's first two convs (yaml rows 0-1: Conv(3, c0, 3, 2) -> Conv(c0, c1, 3, 2), both SiLU) in one
+ * kernel: x NCHW 3-channel f16 / f32 / u8 (as fce_conv2d's stem), y NHWC f16 at a quarter of the input size; the
+ * stem's output stays in LDS.  w / b: the two convs' fce_conv_pack_weights images and BN-folded biases.  Bitwise equal
+ * to the two fce_conv2d calls.  fce_stem_fused_supported: the instantiated (c0, c1).  ABI v6. */
+typedef struct fce_stem2_desc {
+  int c0, c1;
+  const void* w[2];
+  const float* b[2];
+} fce_stem2_desc;
+int fce_stem_fused_supported(const fce_stem2_desc* d);
+int fce_stem_fused(const fce_stem2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
+
 /* ---------------------------------------------------------------- NMS */
 size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 /* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
@@ -295,6 +307,10 @@ int fce_net_set_c3k2_form(fce_net* net, int i, int fused);
  * with the weights of d.  Exactly one form runs; the plan-time autotune keeps the faster (FCE_FUSE_DCLS=1: the fused
  * form).  ABI v6. */
 int fce_net_add_detect_cls_alt(fce_net* net, const fce_dcls_desc* d, int in_buf, int in_coff, int first_op, int nops);
+/* The fused stem pair (fce_stem_fused) as an ALTERNATIVE to the nops (= 2) ops just added: the stem conv reading the
+ * network input and the stride-2 3x3 conv reading all of its output.  fce_net_plan keeps the two convs when any other
+ * op reads the stem's output buffer; otherwise the autotune keeps the faster form (FCE_FUSE_STEM=1: fused).  ABI v6. */
+int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, int nops);
 /* Any alternative op (fused C3k2 or fused Detect cls branch): 1 = the fused form runs, 0 = the ops it replaces run,
  * -1 = op i is not an alternative.  ABI v6. */
 int fce_net_alt_form(const fce_net* net, int i);

@@ -379,6 +379,47 @@ def test_fused_detect_cls_bitwise_equal_to_five_ops(batch, imgsz, tiles, device,
         assert torch.equal(ea(x, graph=False).clone(), yu)
 
 
+@pytest.mark.parametrize("batch,imgsz,dtype,sr,nw", [
+    (2, 320, torch.float16, None, None), (1, 640, torch.float16, "2", "8"), (1, 224, torch.float32, "2", None),
+    (2, 224, torch.uint8, "1", "8"), (1, 224, torch.uint8, None, None), (3, 160, torch.float32, "1", "4")])
+def test_fused_stem_bitwise_equal_to_two_convs(batch, imgsz, dtype, sr, nw, device, monkeypatch):
+    """The one-kernel stem pair (csrc/stem_fused.hip: Conv(3, 16, 3, 2) -> Conv(16, 32, 3, 2), the stem's output in
+    LDS) gives the forward bit for bit what the two convs give, for f16 / f32 / u8 network inputs, both group heights
+    (FCE_STEM2_SR), both block sizes (FCE_STEM2_NW) and partial fragments (224: 56-wide output rows, 160: 40);
+    FCE_FUSE_STEM=1 / 0 / auto as the other
+    alternatives, every form of the auto plan the same forward."""
+    if sr:
+        monkeypatch.setenv("FCE_STEM2_SR", sr)
+    if nw:
+        monkeypatch.setenv("FCE_STEM2_NW", nw)
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(17))
+    x = (x * 255).to(torch.uint8) if dtype == torch.uint8 else x.to(dtype)
+    x = x.to(device)
+    monkeypatch.setenv("FCE_FUSE_STEM", "1")
+    eng = Engine(model, batch, imgsz, device)
+    assert [eng.op_info(i)[0] for i in range(eng.num_ops())].count("stem_fused") == 1
+    yf = eng(x).clone()
+    monkeypatch.setenv("FCE_FUSE_STEM", "0")
+    eng2 = Engine(model, batch, imgsz, device)
+    assert "stem_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
+    yu = eng2(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(yf, yu)
+    monkeypatch.delenv("FCE_FUSE_STEM")
+    ea = Engine(model, batch, imgsz, device)
+    i = [k for k in range(ea.num_ops()) if ea.op_info(k)[0] == "stem_fused"]
+    assert i == [2] and ea.alt_form(2) >= 0
+    for fused in (False, True):
+        ea.set_alt_form(2, fused)
+        assert ea.skipped(0) == ea.skipped(1) == fused != ea.skipped(2)
+        assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
+    # the s scale's stem pair (3 -> 32 -> 64) has no instantiation: its two convs only
+    ms = cases.seeded_model("yolo11s-bifpn.yaml", 0).to(device)
+    es = Engine(ms, 1, 160, device)
+    assert "stem_fused" not in [es.op_info(k)[0] for k in range(es.num_ops())]
+
+
 def test_fused_detect_cls_unknown_tile_is_an_error(device, monkeypatch):
     """FCE_DCLS_TILE_64 / _128 name a tile of that instantiation; anything else fails loudly."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
