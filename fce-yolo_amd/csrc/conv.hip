@@ -1280,6 +1280,160 @@ __global__ __launch_bounds__(256) void conv3x3_ring_kernel(ConvArgs a, int nslot
   }
 }
 
+// ============================================================================ 3x3, persistent, 32x32x16 MFMA
+// The ring above on v_mfma_f32_32x32x16_f16: a wave owns 32 couts x 32 pixels (2 rows x 16 columns) per MFMA, so each
+// B fragment read from LDS (1 KiB: 16 k x 32 pixels) feeds 32 x 32 x 16 MACs instead of 16 x 16 x 32 -- half the LDS
+// bytes per MAC, the ring's bound on the 64 -> 64 convs.  Bitwise identical to the 16x16x32 variants:
+// each 32-deep K-step runs as two 32x32x16 MFMAs over its chunks (4s, 4s+1) then (4s+2, 4s+3), which is how
+// v_mfma_f32_16x16x32_f16 sums a step (profiles/r05_mfma_order.txt: 0 of 200 000 random steps differ).
+// Block: WC waves along the couts (32 each) x WR = 4 / WC along the rows, RPW 2-row pixel tiles per wave: a tile is
+// TH = 2 RPW WR rows x 16 columns, staged like the ring's (swizzled halo image, double-buffered LDS, the next tile's
+// loads issued before this tile's MFMAs).  A: lane l holds cout cb + (l & 31) and chunk 4 s + 2 h + (l >> 5) of
+// K-step s, i.e. lane (l & 15) + 16 (l >> 5) + 32 h of the packed 16x16x32 fragment of cout tile (cb + (l & 31)) / 16.
+// D: register r of lane l is cout cb + 8 (r / 4) + 4 (l >> 5) + r % 4, pixel l & 31.
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+// the double-buffered staged tile of a ring32 configuration fits the 64 KiB of static LDS
+static constexpr bool ring32_fits(int s, int nch, int wc, int rpw) {
+  return wc >= 1 && 2 * ((((2 * rpw * (4 / wc) - 1) * s + 3) * (15 * s + 3) * 4 * nch + 255) / 256) * 256 * 16 <= 64 * 1024;
+}
+
+template <int S, int NCH, int WC, int RPW>
+__global__ __launch_bounds__(256) void conv3x3_ring32_kernel(ConvArgs a, int nslot) {
+  constexpr int WR = 4 / WC, TW = 16, TH = 2 * RPW * WR;
+  constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
+  constexpr int NQ = 4 * NCH, NE = RI * CI * NQ, NL = (NE + 255) / 256, BUF = NL * 256;
+  constexpr int KP = NCH;
+  __shared__ __attribute__((aligned(16))) h8 tile[2 * BUF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wc = wave % WC, wr = wave / WC, hi = lane >> 5;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int by = loc % a.gy, slot = loc / a.gy;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  const int ntiles = tiles_x * tiles_y * a.N;
+  const int chunk = (ntiles + 7) >> 3, tend = min(ntiles, (xcd + 1) * chunk);
+  int t = xcd * chunk + slot;
+  if (t >= tend) return;  // block-uniform
+  const int cb = (by * WC + wc) * 32;  // the wave's first cout
+  const int cotiles = (a.cout + 15) >> 4;
+  h8 af[NCH * 9][2];
+  {
+    const int ct = min((cb + (lane & 31)) >> 4, cotiles - 1);
+    const h8* wf = reinterpret_cast<const h8*>(a.w) + size_t(ct) * a.nalloc * 64 + (lane & 15) + 16 * hi;
+#pragma unroll
+    for (int k = 0; k < NCH * 9; ++k) {
+      af[k][0] = wf[k * 64];
+      af[k][1] = wf[k * 64 + 32];
+    }
+  }
+  float bz[4][4];  // the wave's biases: couts cb + 8 g + 4 hi + j
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[g][j] = bias_or0(a.bias, cb + 8 * g + 4 * hi + j, a.cout);
+  const bool vres = a.res && a.vec_ok;
+  auto stage_load = [&](int tt, h8 (&v)[NL], int (&sl)[NL]) {
+    const int tx = tt % tiles_x, r0 = tt / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
+    const int iy0 = ty * TH * S - 1, ix0 = tx * TW * S - 1;
+    const _Float16* xn = a.x + int64_t(n) * a.Hs * a.Ws * a.xcs;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int pc = e / NQ, q = e - pc * NQ;
+      const int r = pc / CI, c = pc - r * CI;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const int u = r * CI + tile_col<S, CI>(c);
+      sl[i] = e < NE ? u * NQ + tile_slot<KP>(u, q) : e;
+      const bool ok = e < NE && iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws;
+      v[i] = *(ok ? reinterpret_cast<const h8*>(xn + (int64_t(iy) * a.Ws + ix) * a.xcs + q * 8)
+                  : reinterpret_cast<const h8*>(g_zero_line));
+    }
+  };
+  h8 v[NL];
+  int sl[NL];
+  const int step = nslot;
+  stage_load(t, v, sl);
+  for (int cur = 0; t < tend; cur ^= 1) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) tile[cur * BUF + sl[i]] = v[i];
+    __syncthreads();
+    const int tx = t % tiles_x, r0 = t / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
+    // residuals of the wave's outputs (clamped, unconditional), issued before the prefetch: vmcnt retires in order
+    h4 rres[RPW][4];
+    if (vres) {
+#pragma unroll
+      for (int p = 0; p < RPW; ++p) {
+        const int px = lane & 31;
+        const int oy = min(ty * TH + (wr * RPW + p) * 2 + (px >> 4), a.Ho - 1), ox = min(tx * TW + (px & 15), a.Wo - 1);
+        const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          rres[p][g] = *reinterpret_cast<const h4*>(a.res + pix * a.rcs + min(cb + 8 * g + 4 * hi, (a.cout - 4) & ~3));
+      }
+    }
+    stage_load(min(t + step, tend - 1), v, sl);  // unconditional (clamped): see conv3x3_ring_kernel
+    f16v acc[RPW];
+#pragma unroll
+    for (int p = 0; p < RPW; ++p)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[p][j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int p = 0; p < RPW; ++p) {
+          const int px = lane & 31, rr = (wr * RPW + p) * 2 + (px >> 4);
+          const int u = (rr * S + ky) * CI + tile_col<S, CI>((px & 15) * S + kx);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const h8 bf = tile[cur * BUF + u * NQ + tile_slot<KP>(u, k * 4 + 2 * h + hi)];
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[k * 9 + tap][h], bf, acc[p], 0, 0, 0);
+          }
+        }
+      }
+    // epilogue: tile3_post's arithmetic (bias, SiLU, residual, fp16)
+#pragma unroll
+    for (int p = 0; p < RPW; ++p) {
+      const int px = lane & 31;
+      const int oy = ty * TH + (wr * RPW + p) * 2 + (px >> 4), ox = tx * TW + (px & 15);
+      if (oy >= a.Ho || ox >= a.Wo) continue;
+      const int64_t pix = (int64_t(n) * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int co0 = cb + 8 * g + 4 * hi;
+        if (co0 >= a.cout) continue;
+        float vv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float tt = acc[p][4 * g + j] + bz[g][j];
+          vv[j] = a.act ? silu(tt) : tt;
+        }
+        _Float16* yo = static_cast<_Float16*>(a.y) + pix * a.ycs + co0;
+        const bool vec = a.vec_ok && co0 + 3 < a.cout;
+        if (a.res) {
+          if (vec && vres) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vv[j] = fpin(vv[j] + (float)rres[p][g][j]);
+          } else {
+            const _Float16* ro = a.res + pix * a.rcs + co0;
+            for (int j = 0; j < 4; ++j)
+              if (co0 + j < a.cout) vv[j] = fpin(vv[j] + (float)ro[j]);
+          }
+        }
+        if (vec) {
+          *reinterpret_cast<h4*>(yo) = h4{(_Float16)fpin(vv[0]), (_Float16)fpin(vv[1]), (_Float16)fpin(vv[2]), (_Float16)fpin(vv[3])};
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) yo[j] = (_Float16)fpin(vv[j]);
+        }
+      }
+    }
+    t += step;
+  }
+}
+
 // ============================================================================ 3x3, small cin, LDS tiles
 // For cin % 8 == 0 and cin % 32 != 0 (cin <= 64: the C3k2 bottlenecks and early convs of small models,
 // e.g. 8 -> 8 at 160 x 160).  Same block / wave geometry as conv3x3_tile_kernel, but the whole input
@@ -2217,6 +2371,13 @@ static bool no_ring() {  // diagnostics: FCE_NO_RING=1 drops the persistent (rin
   return v;
 }
 
+// the 32x32x16 ring 3x3 candidates (0x900) are opt-in, FCE_RING32=1: on every shape they apply to in the BASELINE
+// models (the 64 -> 64 Detect box 3x3s, the 32 / 64-channel bottlenecks) they ran slower than the 16x16x32 ring,
+// e.g. 33.4 against 23.8 us on n32's P3 box convs (256 VGPRs: one wave per SIMD), profiles/r05_ring32_tune.txt
+static bool no_ring32() {  // read per call, like FCE_WIDE3 (the variant tests switch it on mid-process)
+  const char* e = getenv("FCE_RING32");
+  return !(e && atoi(e) != 0);
+}
 static bool no_gemm3() {  // diagnostics / A-B runs: FCE_NO_GEMM3=1 drops the implicit-GEMM 3x3 candidates (0xC00)
   const char* e = getenv("FCE_NO_GEMM3");
   return e && atoi(e) != 0;
@@ -2289,6 +2450,12 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
     for (int rp : {1, 2, 4})
       for (int pd : {1, 2})
         if (n < cap) out[n++] = 0x600 | (rp << 4) | (pd - 1);
+  if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % 32 == 0 && d.up == 0 && !det_box && !no_ring() &&
+      !no_ring32())  // persistent 32x32x16 ring: 0x900 | rpw << 4 | log2(wc) << 12
+    for (int wcl = 0; wcl < 3; ++wcl)
+      for (int rpw : {1, 2})
+        if (n < cap && ((32 << wcl) >> 1) < d.cout && ring32_fits(d.stride, d.cin / 32, 1 << wcl, rpw))
+          out[n++] = 0x900 | (rpw << 4) | (wcl << 12);
   if (d.k == 3 && d.cin % 32 == 0 && d.up == 0)  // LDS halo-tile kernel: 0x100 | rc | rp << 4 | cw, kp bits
     for (int kp : {1, 2}) {
       if (kp == 2 && d.cin % 64 != 0) continue;
@@ -2470,6 +2637,44 @@ static void launch_ring3_s(const ConvArgs& a, int rp, int pd, dim3 grid, int nsl
   }
 }
 
+
+template <int S, int NCH, int WC, int RPW>
+static void launch_ring32_k(const ConvArgs& a, int ntiles, hipStream_t s) {
+  if constexpr (!ring32_fits(S, NCH, WC, RPW)) {
+    return;  // not a candidate (conv_tile_candidates checks ring32_fits)
+  } else {
+  static const int occ = blocks_per_cu(conv3x3_ring32_kernel<S, NCH, WC, RPW>, 0);
+  const int nslot = ring_slots(ntiles, a.gy, occ);
+  FCE_LAUNCH((conv3x3_ring32_kernel<S, NCH, WC, RPW>), dim3(unsigned(8 * a.gy * nslot)), dim3(256), 0, s, a, nslot);
+  }
+}
+
+template <int S, int NCH>
+static void launch_ring32_s(const ConvArgs& a, int wc, int rpw, int ntiles, hipStream_t s) {
+  if (wc == 1)
+    rpw == 1 ? launch_ring32_k<S, NCH, 1, 1>(a, ntiles, s) : launch_ring32_k<S, NCH, 1, 2>(a, ntiles, s);
+  else if (wc == 2)
+    rpw == 1 ? launch_ring32_k<S, NCH, 2, 1>(a, ntiles, s) : launch_ring32_k<S, NCH, 2, 2>(a, ntiles, s);
+  else
+    rpw == 1 ? launch_ring32_k<S, NCH, 4, 1>(a, ntiles, s) : launch_ring32_k<S, NCH, 4, 2>(a, ntiles, s);
+}
+
+static int launch_ring32(const ConvArgs& a0, int wc, int rpw, int stride, hipStream_t s) {
+  FCE_CHECK((a0.cin == 32 || a0.cin == 64) && a0.cout % 32 == 0 && (wc == 1 || wc == 2 || wc == 4) &&
+                (rpw == 1 || rpw == 2) && (stride == 1 || stride == 2) && ring32_fits(stride, a0.cin / 32, wc, rpw),
+            "conv 3x3 ring32: bad configuration");
+  ConvArgs a = a0;
+  const int th = 2 * rpw * (4 / wc);
+  const int64_t ntiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * a.N;
+  FCE_CHECK(ntiles < (int64_t(1) << 30), "conv 3x3 ring32: too many tiles");
+  a.gy = (a.cout + 32 * wc - 1) / (32 * wc);
+  const int nch = a.cin / 32;
+  if (stride == 1)
+    nch == 1 ? launch_ring32_s<1, 1>(a, wc, rpw, int(ntiles), s) : launch_ring32_s<1, 2>(a, wc, rpw, int(ntiles), s);
+  else
+    nch == 1 ? launch_ring32_s<2, 1>(a, wc, rpw, int(ntiles), s) : launch_ring32_s<2, 2>(a, wc, rpw, int(ntiles), s);
+  return launch_status("conv3x3_ring32_kernel");
+}
 
 // pd: tiles of staged input in flight ahead of the LDS store (1, or 2: two register sets)
 static int launch_ring3(const ConvArgs& a0, int rp, int pd, int stride, hipStream_t s) {
@@ -2753,6 +2958,13 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && out_kind == OUT_F16 && d.up == 0 && (tile & 14) == 0,
               "conv: bad 3x3 ring hint");
     return launch_ring3(a, rp, (tile & 1) ? 2 : 1, d.stride, s);  // 0x601: two tiles of input in flight
+  }
+  if (kind == 9) {  // persistent 3x3 ring on 32x32x16 MFMAs
+    const int rpw = (tile >> 4) & 15, wc = 1 << ((tile >> 12) & 3);
+    FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % 32 == 0 && out_kind == OUT_F16 && d.up == 0 &&
+                  (tile & 0xF) == 0,
+              "conv: bad 3x3 ring32 hint");
+    return launch_ring32(a, wc, rpw, d.stride, s);
   }
   if (kind == 8) {  // big-tile LDS-DMA 3x3 kernel
     const int wm = (tile >> 4) & 15, ab = ((tile >> 12) & 1) + 2, nw = 4;

@@ -1056,6 +1056,9 @@ CONV_VARIANT_CASES = [  # cin, cout, k, stride, H, W, residual
     (128, 136, 3, 2, 41, 37, False), (96, 192, 3, 2, 33, 47, True), (64, 96, 3, 1, 19, 35, True),
     # 256-wide implicit-GEMM 3x3 (0xCx0): stride 2 over odd maps with partial pixel tiles, residual, 512 couts
     (512, 256, 3, 2, 21, 19, True), (64, 512, 3, 1, 13, 11, False),
+    # persistent 32x32x16 ring 3x3 (0x9x0): cin 32 / 64, stride 1 / 2, partial row / column tiles, residual, 32 couts
+    (32, 32, 3, 1, 9, 50, True), (64, 128, 3, 2, 19, 33, True), (64, 64, 3, 2, 21, 37, False),
+    (32, 96, 3, 1, 23, 17, False),
 ]
 
 
@@ -1134,6 +1137,7 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     within the per-op tolerance."""
     monkeypatch.setenv("FCE_TILE3AL", "1")
     monkeypatch.setenv("FCE_WIDE3", "1")  # + the opt-in wide-tile 3x3 (0xA00)
+    monkeypatch.setenv("FCE_RING32", "1")  # + the opt-in 32x32x16 ring 3x3 (0x900)
     cin, cout, k, stride, H, W, with_res = case
     g = torch.Generator().manual_seed(cin * 1000 + cout)
     w = torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)
@@ -1155,6 +1159,15 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     codes = (C.c_int * 128)()
     nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     assert nv >= 2
+    # the 32x32x16 ring is offered exactly where one of its tiles applies (its sums are the 16x16x32 kernels', bit for
+    # bit): cin 32 / 64, cout % 32 == 0, a double-buffered tile within 64 KiB of static LDS, more couts than half a group
+    def ring32_fits(wc, rpw):
+        ne = (((2 * rpw * (4 // wc) - 1) * stride + 3) * (15 * stride + 3) * 4 * (cin // 32) + 255) // 256 * 256
+        return 2 * ne * 16 <= 64 * 1024
+
+    offered = k == 3 and cin in (32, 64) and cout % 32 == 0 and any(
+        ring32_fits(wc, rpw) and 16 * wc < cout for wc in (1, 2, 4) for rpw in (1, 2))
+    assert any((codes[i] & 0xF00) == 0x900 for i in range(nv)) == offered
     outs = {}
     for code in [-1] + list(codes[:nv]):
         y = torch.full((2, Ho, Wo, cout), float("nan"), dtype=torch.float16, device=device)
