@@ -40,8 +40,11 @@ struct StG {
   static constexpr int NS = 2 * SR2 + 1;  // stem rows
   static constexpr int K1 = C0 / 8, sS = K1 | 1;  // stem chunks per position, LDS units per position (odd)
   static constexpr int RC0 = C0 / 16, CT1 = C1 / 16;
-  static constexpr int NS1 = (9 * K1 + 3) / 4;  // second conv K-steps (dense_geom)
-  static_assert(C0 % 16 == 0 && C1 % 16 == 0 && C0 % 32 != 0, "stem fused: channel configuration");
+  // second conv K-steps as conv_pack orders them: chunk-major (32-channel chunk, tap) for c0 % 32 == 0, else
+  // tap-major 8-channel chunks
+  static constexpr bool CM = C0 % 32 == 0;
+  static constexpr int NS1 = CM ? 9 * (C0 / 32) : (9 * K1 + 3) / 4;
+  static_assert(C0 % 16 == 0 && C1 % 16 == 0, "stem fused: channel configuration");
 };
 
 // 8 consecutive input elements, raw (a prefetch register image: converted to fp16 only when written to LDS, so the
@@ -206,10 +209,20 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_fused_kernel(Stem2Args a) {
       for (int ct = 0; ct < G::CT1; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < G::NS1; ++st) {
-        const int c = st * 4 + grp;  // tap-major 8-channel chunk
+        int tap, cc;
+        bool ok;
+        if (G::CM) {  // chunk-major: step = (32-channel chunk) * 9 + tap
+          tap = st % 9;
+          cc = (st / 9) * 4 + grp;
+          ok = true;
+        } else {  // tap-major 8-channel chunk c = 4 st + grp
+          const int c = st * 4 + grp;
+          tap = c / G::K1;
+          cc = c - tap * G::K1;
+          ok = c < 9 * G::K1;
+        }
         h8 b = h8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (c < 9 * G::K1) {
-          const int tap = c / G::K1, cc = c - tap * G::K1;
+        if (ok) {
           const int ky = tap / 3, kx = tap - ky * 3;
           const int cp = 2 * oxc + kx, p = (cp & 1) ? half + (cp >> 1) : (cp >> 1);
           b = S[((2 * r1 + ky) * npos + p) * G::sS + cc];
@@ -233,10 +246,12 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_fused_kernel(Stem2Args a) {
 }
 
 // ============================================================================ host
-// (c0, c1) instantiated: the n scale's 3 -> 16 -> 32 (s, m, l have c0 % 32 == 0 or other widths: their two convs
-// stay separate).  FCE_STEM2_SR = 1 / 2 output rows per group (default 2), FCE_STEM2_NW = 4 / 8 waves (default 8; n32 pipelined
-// bench 38.5k images/s against 38.1k with 1 row / 4 waves and 37.7k unfused, profiles/r05_stem_ab.txt).
-static constexpr int kStemInsts[][2] = {{16, 32}};
+// (c0, c1) instantiated: the n scale's 3 -> 16 -> 32 and the s scale's 3 -> 32 -> 64 (m at 1280 and l's 64-channel
+// stem do not fit the LDS tile / the register-resident fragments: their two convs stay separate).
+// FCE_STEM2_SR = 1 / 2 output rows per group, FCE_STEM2_NW = 4 / 8 waves: n default 2 rows x 8 waves (n32 pipelined
+// bench 38.5k images/s against 38.1k with 1 row / 4 waves and 37.7k unfused, profiles/r05_stem_ab.txt), s 1 x 4 (two
+// rows of the 32-channel stem image do not fit 160 KiB; eight waves spill at the 256-register cap).
+static constexpr int kStemInsts[][2] = {{16, 32}, {32, 64}};
 
 bool stem_fused_ok(const fce_stem2_desc& d) {
   for (const auto& s : kStemInsts)
@@ -272,15 +287,20 @@ static int st_launch(const Stem2Args& a, hipStream_t s) {
 }
 
 template <typename T>
-static int st_dispatch(const Stem2Args& a, hipStream_t s) {
+static int st_dispatch(const Stem2Args& a, int c0, hipStream_t s) {
   const char* e = getenv("FCE_STEM2_SR");  // read per call: tests switch it
   const char* w = getenv("FCE_STEM2_NW");
-  const int sr = e && *e ? atoi(e) : 2, nw = w && *w ? atoi(w) : 8;
-  if (sr == 1 && nw == 4) return st_launch<T, 16, 32, 1, 4>(a, s);
-  if (sr == 1 && nw == 8) return st_launch<T, 16, 32, 1, 8>(a, s);
-  if (sr == 2 && nw == 4) return st_launch<T, 16, 32, 2, 4>(a, s);
-  if (sr == 2 && nw == 8) return st_launch<T, 16, 32, 2, 8>(a, s);
-  return fail(FCE_ERR_INVALID, "FCE_STEM2_SR / FCE_STEM2_NW: 1 or 2 rows, 4 or 8 waves");
+  const int sr = e && *e ? atoi(e) : (c0 == 16 ? 2 : 1), nw = w && *w ? atoi(w) : (c0 == 16 ? 8 : 4);
+  if (c0 == 16) {
+    if (sr == 1 && nw == 4) return st_launch<T, 16, 32, 1, 4>(a, s);
+    if (sr == 1 && nw == 8) return st_launch<T, 16, 32, 1, 8>(a, s);
+    if (sr == 2 && nw == 4) return st_launch<T, 16, 32, 2, 4>(a, s);
+    if (sr == 2 && nw == 8) return st_launch<T, 16, 32, 2, 8>(a, s);
+  } else {
+    if (sr == 1 && nw == 4) return st_launch<T, 32, 64, 1, 4>(a, s);
+    if (sr == 1 && nw == 8) return st_launch<T, 32, 64, 1, 8>(a, s);
+  }
+  return fail(FCE_ERR_INVALID, "FCE_STEM2_SR / FCE_STEM2_NW: 1 or 2 rows (1 for c0 32), 4 or 8 waves");
 }
 
 int stem_fused(const fce_stem2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s) {
@@ -306,9 +326,9 @@ int stem_fused(const fce_stem2_desc& d, const fce_tensor& x, const fce_tensor& y
   a.b1 = d.b[1];
   a.y = static_cast<_Float16*>(y.data) + y.coff;
   a.ycs = y.cstride;
-  if (x.dtype == FCE_F16) return st_dispatch<_Float16>(a, s);
-  if (x.dtype == FCE_F32) return st_dispatch<float>(a, s);
-  if (x.dtype == FCE_U8) return st_dispatch<uint8_t>(a, s);
+  if (x.dtype == FCE_F16) return st_dispatch<_Float16>(a, d.c0, s);
+  if (x.dtype == FCE_F32) return st_dispatch<float>(a, d.c0, s);
+  if (x.dtype == FCE_U8) return st_dispatch<uint8_t>(a, d.c0, s);
   return fail(FCE_ERR_INVALID, "stem fused: input dtype");
 }
 

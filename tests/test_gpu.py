@@ -379,12 +379,15 @@ def test_fused_detect_cls_bitwise_equal_to_five_ops(batch, imgsz, tiles, device,
         assert torch.equal(ea(x, graph=False).clone(), yu)
 
 
-@pytest.mark.parametrize("batch,imgsz,dtype,sr,nw", [
-    (2, 320, torch.float16, None, None), (1, 640, torch.float16, "2", "8"), (1, 224, torch.float32, "2", None),
-    (2, 224, torch.uint8, "1", "8"), (1, 224, torch.uint8, None, None), (3, 160, torch.float32, "1", "4")])
-def test_fused_stem_bitwise_equal_to_two_convs(batch, imgsz, dtype, sr, nw, device, monkeypatch):
-    """The one-kernel stem pair (csrc/stem_fused.hip: Conv(3, 16, 3, 2) -> Conv(16, 32, 3, 2), the stem's output in
-    LDS) gives the forward bit for bit what the two convs give, for f16 / f32 / u8 network inputs, both group heights
+@pytest.mark.parametrize("cfg,batch,imgsz,dtype,sr,nw", [
+    ("yolo11n-fce.yaml", 2, 320, torch.float16, None, None), ("yolo11n-fce.yaml", 1, 640, torch.float16, "2", "8"),
+    ("yolo11n-fce.yaml", 1, 224, torch.float32, "2", None), ("yolo11n-fce.yaml", 2, 224, torch.uint8, "1", "8"),
+    ("yolo11n-fce.yaml", 1, 224, torch.uint8, None, None), ("yolo11n-fce.yaml", 3, 160, torch.float32, "1", "4"),
+    ("yolo11s-bifpn.yaml", 2, 256, torch.float16, None, None), ("yolo11s-bifpn.yaml", 1, 224, torch.uint8, "1", "8")])
+def test_fused_stem_bitwise_equal_to_two_convs(cfg, batch, imgsz, dtype, sr, nw, device, monkeypatch):
+    """The one-kernel stem pair (csrc/stem_fused.hip: Conv(3, 16, 3, 2) -> Conv(16, 32, 3, 2) of the n scale, 3 -> 32 ->
+    64 of the s scale with the chunk-major K order, the stem's output in LDS) gives the forward bit for bit what the
+    two convs give, for f16 / f32 / u8 network inputs, both group heights
     (FCE_STEM2_SR), both block sizes (FCE_STEM2_NW) and partial fragments (224: 56-wide output rows, 160: 40);
     FCE_FUSE_STEM=1 / 0 / auto as the other
     alternatives, every form of the auto plan the same forward."""
@@ -392,7 +395,7 @@ def test_fused_stem_bitwise_equal_to_two_convs(batch, imgsz, dtype, sr, nw, devi
         monkeypatch.setenv("FCE_STEM2_SR", sr)
     if nw:
         monkeypatch.setenv("FCE_STEM2_NW", nw)
-    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    model = cases.seeded_model(cfg, 0).to(device)
     x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(17))
     x = (x * 255).to(torch.uint8) if dtype == torch.uint8 else x.to(dtype)
     x = x.to(device)
@@ -414,10 +417,10 @@ def test_fused_stem_bitwise_equal_to_two_convs(batch, imgsz, dtype, sr, nw, devi
         ea.set_alt_form(2, fused)
         assert ea.skipped(0) == ea.skipped(1) == fused != ea.skipped(2)
         assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
-    # the s scale's stem pair (3 -> 32 -> 64) has no instantiation: its two convs only
-    ms = cases.seeded_model("yolo11s-bifpn.yaml", 0).to(device)
-    es = Engine(ms, 1, 160, device)
-    assert "stem_fused" not in [es.op_info(k)[0] for k in range(es.num_ops())]
+    # the l scale's stem pair (3 -> 64 -> 128) has no instantiation: its two convs only
+    ml = cases.seeded_model("yolo11l-fce.yaml", 0).to(device)
+    el = Engine(ml, 1, 160, device)
+    assert "stem_fused" not in [el.op_info(k)[0] for k in range(el.num_ops())]
 
 
 def test_fused_detect_cls_unknown_tile_is_an_error(device, monkeypatch):
