@@ -55,7 +55,11 @@ struct DcG {
   static constexpr int OP = OB + (NB + 3) / 4;
   static constexpr int PSZ = dc_max(R1 * s1, NC * s3);
   static constexpr int OQ = OP + PSZ;
-  static constexpr int QSZ = dc_max(dc_max(XR * sX, R1 * s3), NC * s3);
+  // x and t2 are the depthwise stages' inputs: staged as fp32 (the fp16 values, converted once) in two planes, the
+  // low and high 4 channels of each 8-channel chunk, so a thread's 8 channels are two conflict-free 16-byte reads and
+  // the taps run as v_pk_fma_f32 (two exact fmas per instruction, the same values as v_fma_mix)
+  static constexpr int QX = XR * K0, QT = R1 * K3;  // units per plane
+  static constexpr int QSZ = dc_max(dc_max(2 * QX, 2 * QT), NC * s3);
   static constexpr int TOTAL = OQ + QSZ;
   static constexpr size_t LDS = size_t(TOTAL) * 16;
   static constexpr int NXE = (XR * K0 + NT - 1) / NT;  // x chunks per thread
@@ -88,25 +92,36 @@ __device__ __forceinline__ void dc_tile(const DclsArgs& a, int TH, int TW, int t
   x0 = tx * TW;
 }
 
-// depthwise 3x3 (stride 1) of one 8-channel chunk at one output position from an LDS image: dwconv_kernel's order
-// (acc = bias, (ky, kx) order, rows outside the image skipped, every column of a kept row fused, zeros outside),
-// then SiLU and fp16.  (A taps-outermost form over several positions per thread, which let a 16-wave block fit
-// 128 VGPRs, measured slower: 86.6 against 81.7 us on n32's P3, 132 us with 16 waves, DESIGN.md.)
-__device__ __forceinline__ h8 dc_dw(const h8* img, int p00, int rw, int stride, int ch, int iy, int H,
+// depthwise 3x3 (stride 1) of one 8-channel chunk at one output position from an fp32 LDS image (planes lo / hi of
+// `plane` units each, position stride k chunks): dwconv_kernel's order (acc = bias, (ky, kx) order, rows outside the
+// image skipped, every column of a kept row fused, zeros outside), each tap as four v_pk_fma_f32 -- fma(x, w, acc)
+// with the exactly converted fp16 x, as v_fma_mix computes it -- then SiLU and fp16.  (A taps-outermost form over
+// several positions per thread, which let a 16-wave block fit 128 VGPRs, measured slower: 86.6 against 81.7 us on
+// n32's P3, 132 us with 16 waves, DESIGN.md.)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h8 dc_dw(const f4* img, int plane, int p00, int rw, int k, int ch, int iy, int H,
                                     const float (&wk)[9][8], const float (&bz)[8]) {
-  float acc[8];
+  f2 acc[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = bz[j];
+  for (int j = 0; j < 4; ++j) acc[j] = f2{bz[2 * j], bz[2 * j + 1]};
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky) {
     const int yy = iy - 1 + ky;
     if (yy < 0 || yy >= H) continue;
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) fma8_mix(img[(p00 + ky * rw + kx) * stride + ch], wk[ky * 3 + kx], acc);
+    for (int kx = 0; kx < 3; ++kx) {
+      const int u = (p00 + ky * rw + kx) * k + ch;
+      const f4 lo = img[u], hi = img[plane + u];
+      const float* w = wk[ky * 3 + kx];
+      acc[0] = __builtin_elementwise_fma(f2{lo[0], lo[1]}, f2{w[0], w[1]}, acc[0]);
+      acc[1] = __builtin_elementwise_fma(f2{lo[2], lo[3]}, f2{w[2], w[3]}, acc[1]);
+      acc[2] = __builtin_elementwise_fma(f2{hi[0], hi[1]}, f2{w[4], w[5]}, acc[2]);
+      acc[3] = __builtin_elementwise_fma(f2{hi[2], hi[3]}, f2{w[6], w[7]}, acc[3]);
+    }
   }
   h8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(silu(acc[j]));
+  for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(silu(acc[j >> 1][j & 1]));
   return o;
 }
 
@@ -183,6 +198,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
   h8* P = sm + G::OP;
   h8* Q = sm + G::OQ;
   _Float16* Qh = reinterpret_cast<_Float16*>(Q);
+  f4* Qf = reinterpret_cast<f4*>(Q);
   const h8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t clk[7] = {0, 0, 0, 0, 0, 0, 0}, tprev = a.diag ? __builtin_amdgcn_s_memtime() : 0;
   auto tick = [&](int k) {
@@ -200,7 +216,11 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
 #pragma unroll
     for (int k = 0; k < G::NXE; ++k) {
       const int e = tid + k * G::NT, pos = e / G::K0;
-      if (pos < G::XR) Q[pos * G::sX + (e - pos * G::K0)] = xr[k];
+      if (pos < G::XR) {
+        const h8 v = xr[k];
+        Qf[e] = f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        Qf[G::QX + e] = f4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+      }
     }
     tick(0);
     if (t + 1 < t_end) load_x(t + 1);
@@ -215,7 +235,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
         const int r = pos / G::RW, c = pos - r * G::RW;
         const int iy = y0 - 1 + r, ix = x0 - 1 + c;
         h8 o = zero8;  // outside the image: unused (pw1 zeroes t2 there)
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) o = dc_dw(Q, r * G::XW + c, G::XW, G::sX, ch, iy, a.H, wk, bz);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) o = dc_dw(Qf, G::QX, r * G::XW + c, G::XW, G::K0, ch, iy, a.H, wk, bz);
         P[pos * G::s1 + ch] = o;
       }
     }
@@ -238,9 +258,10 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu(acc[j] + bias[G::BP1 + co0 + j]);
-        h4 o = h4_of(v);
-        if (!(iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)) o = h4{0, 0, 0, 0};
-        *reinterpret_cast<h4*>(Qh + (q * G::s3) * 8 + co0) = o;
+        const h4 o = h4_of(v);  // t2 is stored as the fp32 values of its fp16 rounding (zero outside the image)
+        const bool in = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        Qf[(co0 & 4 ? G::QT : 0) + q * G::K3 + (co0 >> 3)] =
+            in ? f4{(float)o[0], (float)o[1], (float)o[2], (float)o[3]} : f4{0.f, 0.f, 0.f, 0.f};
       };
       mfma_stage<G::MF1, G::CT3, G::NS1>(sm + lane, bl, epi);
     }
@@ -255,7 +276,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
         const int r = pos / TW, c = pos - r * TW;
         const int iy = y0 + r, ix = x0 + c;
         h8 o = zero8;  // outside the image: never stored
-        if (iy < a.H && ix < a.W) o = dc_dw(Q, r * G::RW + c, G::RW, G::s3, ch, iy, a.H, wk, bz);
+        if (iy < a.H && ix < a.W) o = dc_dw(Qf, G::QT, r * G::RW + c, G::RW, G::K3, ch, iy, a.H, wk, bz);
         P[pos * G::s3 + ch] = o;
       }
     }
