@@ -47,6 +47,7 @@ bool c3k2_fused_ok(const fce_c3k2_desc& d);
 int c3k2_fused(const fce_c3k2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 bool detect_cls_fused_ok(const fce_dcls_desc& d);
 bool stem_fused_ok(const fce_stem2_desc& d);
+bool stem_fused_fits(const fce_stem2_desc& d, int h, int w);
 int stem_fused(const fce_stem2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_detect_epi& e, hipStream_t s);
 
@@ -1197,10 +1198,12 @@ int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags) {
     }
     net->anchors = A;
     net->ws_bytes = ws;
-    // a fused stem pair skips writing the stem's output: valid only when nothing but the second conv reads it
+    // a fused stem pair skips writing the stem's output: valid only when nothing but the second conv reads it, and
+    // only for the input sizes its kernel is built for
     for (size_t i = 0; i < net->ops.size(); ++i) {
       OpDesc& op = net->ops[i];
-      if (op.kind != OP_STEM2 || op.alt_first < 0 || op.alt_locked) continue;
+      if (op.kind != OP_STEM2 || op.alt_first < 0) continue;
+      op.alt_locked = !stem_fused_fits(op.stem2, h, w);
       const OpDesc& s0 = net->ops[op.alt_first];
       std::vector<Access> acc;
       for (size_t j = 0; j < net->ops.size() && !op.alt_locked; ++j) {

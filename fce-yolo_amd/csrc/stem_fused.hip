@@ -259,6 +259,10 @@ bool stem_fused_ok(const fce_stem2_desc& d) {
   return false;
 }
 
+// the planned input size fits the kernel: the register image of the staged rows is sized for W <= 640 (and the
+// LDS tile with it); the executor keeps the two convs otherwise
+bool stem_fused_fits(const fce_stem2_desc& d, int h, int w) { return stem_fused_ok(d) && h > 0 && w % 8 == 0 && w <= 640; }
+
 template <typename T, int C0, int C1, int SR2, int NW>
 static int st_launch(const Stem2Args& a, hipStream_t s) {
   using G = StG<C0, C1, SR2>;

@@ -423,6 +423,23 @@ def test_fused_stem_bitwise_equal_to_two_convs(cfg, batch, imgsz, dtype, sr, nw,
     assert "stem_fused" not in [el.op_info(k)[0] for k in range(el.num_ops())]
 
 
+def test_fused_stem_kept_out_where_it_does_not_fit(device, monkeypatch):
+    """The fused stem pair is built for input widths <= 640: at 704 the plan keeps the two convs (locked: the fused form
+    cannot be selected, not even with FCE_FUSE_STEM=1), and the forward equals the one without the alternative."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    x = torch.rand(1, 3, 704, 704, generator=torch.Generator().manual_seed(5)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_STEM", "1")
+    eng = Engine(model, 1, 704, device)
+    assert eng.op_info(2)[0] == "stem_fused" and eng.alt_form(2) == 0 and not eng.skipped(0) and eng.skipped(2)
+    with pytest.raises(RuntimeError, match="cannot run"):
+        eng.set_alt_form(2, True)
+    y = eng(x).clone()
+    monkeypatch.setenv("FCE_FUSE_STEM", "0")
+    y0 = Engine(model, 1, 704, device)(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+
+
 def test_fused_detect_cls_unknown_tile_is_an_error(device, monkeypatch):
     """FCE_DCLS_TILE_64 / _128 name a tile of that instantiation; anything else fails loudly."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
