@@ -1377,9 +1377,9 @@ int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* m
 
 int fce_net_op_info(const fce_net* net, int i, char* name, int cap, double* bytes, double* flops) {
   FCE_CHECK(net && i >= 0 && i < int(net->ops.size()) && bytes && flops, "fce_net_op_info: bad argument");
-  FCE_CHECK(net->batch > 0, "fce_net_op_info: plan first");
   std::string nm;
   op_cost(net, net->ops[i], &nm, bytes, flops);
+  if (net->batch <= 0) *bytes = *flops = 0;  // before fce_net_plan: the op's name only (no sizes yet)
   if (name && cap > 0) {
     size_t n = std::min(nm.size(), size_t(cap - 1));
     nm.copy(name, n);

@@ -353,7 +353,8 @@ int fce_net_wait_fork(fce_net* net, void* stream);
 int fce_net_profile(fce_net* net, const fce_tensor* input, float* pred, float* ms, int* launches, int cap,
                     void* stream);
 int fce_net_num_ops(const fce_net* net);
-/* name (kernel family), algorithmic bytes and flops of op i at the planned size */
+/* name (kernel family), algorithmic bytes and flops of op i at the planned size (before fce_net_plan: the name,
+ * zero bytes and flops) */
 int fce_net_op_info(const fce_net* net, int i, char* name, int name_cap, double* bytes, double* flops);
 int fce_net_buffer(const fce_net* net, int id, fce_tensor* out);
 /* kernel variant code the plan-time autotune chose for op i (-1 = heuristic / not tunable) */

@@ -268,3 +268,55 @@ def test_bench_world_size_mismatch_fails():
     r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "4"], capture_output=True, text=True,
                        timeout=300, env=_bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
     assert r.returncode != 0 and "WORLD_SIZE 2" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+def _lowered(cfg, monkeypatch, **env):
+    """A model lowered into a NetBackend on the CPU (ops recorded, never planned or run): [(name, alt_form)]."""
+    from fce_yolo_amd.backend import NetBackend
+
+    for k in ("FCE_FUSE_STEM", "FCE_FUSE_DCLS", "FCE_FUSE_C3K2"):
+        if k in env:
+            monkeypatch.setenv(k, env[k])
+        else:
+            monkeypatch.delenv(k, raising=False)
+    model = cases.seeded_model(cfg, 0)
+    be = NetBackend(640, 640, torch.device("cpu"))
+    try:
+        with torch.no_grad():
+            model.emit(be, be.input_view(1, 3))
+        L = N.lib()
+        out = []
+        for i in range(L.fce_net_num_ops(be.net)):
+            name = C.create_string_buffer(64)
+            nb, fl = C.c_double(), C.c_double()
+            N.call("fce_net_op_info", be.net, i, name, 64, C.byref(nb), C.byref(fl))
+            out.append((name.value.decode(), L.fce_net_alt_form(be.net, i)))
+        return out
+    finally:
+        be.close()
+
+
+def test_lowering_records_the_fused_alternatives(monkeypatch):
+    """Graph lowering (no GPU): the n scale records the one-kernel stem pair after its two convs, the fused C3k2 after
+    each qualifying block's four convs, and per Detect level P3 / P4 the box tail before the cls chain, whose five ops
+    are followed by their one-kernel alternative; every alternative starts in its fused form (the plan decides).  The
+    FCE_FUSE_* switches drop them; the s scale gets the stem pair but not the cls branch (c3 128), the l scale
+    neither."""
+    ops = _lowered("yolo11n-fce.yaml", monkeypatch)
+    names = [n for n, _ in ops]
+    alts = [(i, n) for i, (n, f) in enumerate(ops) if f >= 0]
+    assert all(ops[i][1] == 1 for i, _ in alts)
+    assert [n for _, n in alts] == ["stem_fused"] + ["c3k2_fused"] * 3 + ["detect_cls_fused"] * 2
+    assert names[:3] == ["conv_stem", "conv3x3_mfma", "stem_fused"]
+    for i, n in alts:
+        if n == "detect_cls_fused":
+            assert names[i - 5:i] == ["dwconv3x3", "conv1x1_mfma", "dwconv3x3", "conv1x1_mfma", "conv1x1_detect_cls"]
+            assert names[i - 6] == "conv1x1_detect_box"
+        if n == "c3k2_fused":
+            assert names[i - 4:i] == ["conv1x1_mfma", "conv3x3_mfma", "conv3x3_mfma", "conv1x1_mfma"]
+    plain = _lowered("yolo11n-fce.yaml", monkeypatch, FCE_FUSE_STEM="0", FCE_FUSE_DCLS="0", FCE_FUSE_C3K2="0")
+    assert all(f < 0 for _, f in plain) and len(plain) == len(ops) - len(alts)
+    s_ops = [n for n, f in _lowered("yolo11s-bifpn.yaml", monkeypatch) if f >= 0]
+    assert "stem_fused" in s_ops and "detect_cls_fused" not in s_ops
+    l_ops = [n for n, f in _lowered("yolo11l-fce.yaml", monkeypatch) if f >= 0]
+    assert "stem_fused" not in l_ops and "detect_cls_fused" not in l_ops
