@@ -101,7 +101,7 @@ __device__ __forceinline__ void c3_tile(const C3k2Args& a, int TH, int TW, int t
   x0 = tx * TW;
 }
 
-template <int CIN, int C, int CM, int COUT, int TH, int TW, int NW>
+template <int CIN, int C, int CM, int COUT, int TH, int TW, int NW, bool YB>
 __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
   using G = C3G<CIN, C, CM, COUT, TH, TW, NW>;
   extern __shared__ __attribute__((aligned(16))) h8 sm[];
@@ -260,15 +260,21 @@ __global__ __launch_bounds__(NW * 64, 2) void c3k2_fused_kernel(C3k2Args a) {
         if (cc >= 3 * C / 8) return h8{0, 0, 0, 0, 0, 0, 0, 0};
         return cc < 2 * C / 8 ? Tin[pt[i] + cc] : Min[pm[i] + cc];
       };
+      // YB: y through a per-image buffer resource, every lane storing (store_h4_or_drop), so the next tile's
+      // stage 1 waits for its x prefetch only, not for these stores; otherwise branched global stores
+      const uint32_t img = uint32_t(a.H) * uint32_t(a.W) * uint32_t(a.ycs);
+      const __amdgpu_buffer_rsrc_t yr = out_rsrc(a.y + int64_t(n) * img, img * 2u);
       auto epi = [&](int i, int ct, const f4& acc) {
         const int q = (wave + NW * i) * 16 + col;
-        if (q >= G::NC || ct * 16 + grp * 4 >= COUT) return;
         const int r = q / TW, cq = q - r * TW;
         const int iy = y0 + r, ix = x0 + cq;
-        if (iy >= a.H || ix >= a.W) return;
+        const bool ok = q < G::NC && ct * 16 + grp * 4 < COUT && iy < a.H && ix < a.W;
+        if (!YB && !ok) return;
         float v[4];
         c3_act(bias + G::B4, ct, grp, acc, v);
-        *reinterpret_cast<h4*>(a.y + nhwc_off(n, iy, ix, a.H, a.W, a.ycs) + ct * 16 + grp * 4) = h4_of(v);
+        const int off = (iy * a.W + ix) * a.ycs + ct * 16 + grp * 4;
+        if constexpr (YB) store_h4_or_drop(yr, ok, uint32_t(off) * 2u, h4_of(v));
+        else *reinterpret_cast<h4*>(a.y + int64_t(n) * img + off) = h4_of(v);
       };
       mfma_stage<G::MF4, G::CT4, G::NS4>(sm + G::OW4 + lane, bl, epi);
     }
@@ -294,11 +300,11 @@ struct C3Inst {
 };
 static constexpr C3Inst kC3Insts[] = {{32, 16, 8, 64}, {64, 32, 16, 128}, {32, 32, 16, 64}};
 
-template <int CIN, int C, int CM, int COUT, int TH, int TW, int NW>
+template <int CIN, int C, int CM, int COUT, int TH, int TW, int NW, bool YB>
 static int c3_launch(const C3k2Args& a0, int H, int W, int N, hipStream_t s) {
   using G = C3G<CIN, C, CM, COUT, TH, TW, NW>;
   static_assert(G::LDS <= 160 * 1024, "c3k2 fused: LDS over 160 KiB");
-  auto k = c3k2_fused_kernel<CIN, C, CM, COUT, TH, TW, NW>;
+  auto k = c3k2_fused_kernel<CIN, C, CM, COUT, TH, TW, NW, YB>;
   static const bool big = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!big && G::LDS > 64 * 1024) return fail(FCE_ERR_HIP, "c3k2 fused: cannot opt in to >64 KiB LDS");
@@ -341,7 +347,18 @@ static int c3_launch_cfg(const C3k2Args& a, int H, int W, int N, hipStream_t s) 
     else if (strcmp(env, "4,40,8") == 0) wide = false;
     else return fail(FCE_ERR_INVALID, "FCE_C3K2_TILE: only \"8,16,4\" or \"4,40,8\"");
   }
-  return wide ? c3_launch<CIN, C, CM, COUT, 8, 16, 4>(a, H, W, N, s) : c3_launch<CIN, C, CM, COUT, 4, 40, 8>(a, H, W, N, s);
+  // y stores: through a buffer resource, every lane storing, for the cout-64 blocks (n L2 73.1 against 75.7 us,
+  // L18 44.1 against 44.5); branched global stores for cout 128 (n L4 53.4 against 56.0 us;
+  // profiles/r05_c3k2_ystore_ab.txt).  FCE_C3K2_YSTORE=buf / global forces one (A/B runs); any other value is an error
+  const char* yst = getenv("FCE_C3K2_YSTORE");
+  bool yb = COUT <= 64;
+  if (yst && *yst) {
+    if (strcmp(yst, "buf") == 0) yb = true;
+    else if (strcmp(yst, "global") == 0) yb = false;
+    else return fail(FCE_ERR_INVALID, "FCE_C3K2_YSTORE: only \"buf\" or \"global\"");
+  }
+  if (wide) return yb ? c3_launch<CIN, C, CM, COUT, 8, 16, 4, true>(a, H, W, N, s) : c3_launch<CIN, C, CM, COUT, 8, 16, 4, false>(a, H, W, N, s);
+  return yb ? c3_launch<CIN, C, CM, COUT, 4, 40, 8, true>(a, H, W, N, s) : c3_launch<CIN, C, CM, COUT, 4, 40, 8, false>(a, H, W, N, s);
 }
 
 static int c3_inst(const fce_c3k2_desc& d) {

@@ -293,20 +293,32 @@ def test_fused_c3k2_unknown_tile_is_an_error(device, monkeypatch):
         eng = Engine(model, 1, 160, device)
         eng(x)
         torch.cuda.synchronize()
+    monkeypatch.delenv("FCE_C3K2_TILE")
+    monkeypatch.setenv("FCE_C3K2_YSTORE", "lds")
+    with pytest.raises(RuntimeError, match="FCE_C3K2_YSTORE"):
+        eng = Engine(model, 1, 160, device)
+        eng(x)
+        torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("cfg,batch,imgsz,tile", [
-    ("yolo11n-fce.yaml", 2, 320, None), ("yolo11s-bifpn.yaml", 2, 256, None), ("yolo11n-fce.yaml", 1, 640, None),
-    ("yolo11n-fce.yaml", 1, 224, None), ("yolo11n-fce.yaml", 1, 224, "8,16,4"), ("yolo11n-fce.yaml", 1, 224, "4,40,8"),
-    ("yolo11n-fce.yaml", 2, 160, "4,40,8")])
-def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, device, monkeypatch):
+@pytest.mark.parametrize("cfg,batch,imgsz,tile,ystore", [
+    ("yolo11n-fce.yaml", 2, 320, None, None), ("yolo11s-bifpn.yaml", 2, 256, None, None),
+    ("yolo11n-fce.yaml", 1, 640, None, None), ("yolo11n-fce.yaml", 1, 224, None, None),
+    ("yolo11n-fce.yaml", 1, 224, "8,16,4", None), ("yolo11n-fce.yaml", 1, 224, "4,40,8", None),
+    ("yolo11n-fce.yaml", 2, 160, "4,40,8", None), ("yolo11n-fce.yaml", 1, 224, None, "buf"),
+    ("yolo11n-fce.yaml", 1, 224, None, "global"), ("yolo11s-bifpn.yaml", 1, 224, "4,40,8", "buf")])
+def test_fused_c3k2_bitwise_equal_to_four_convs(cfg, batch, imgsz, tile, ystore, device, monkeypatch):
     """The fused C3k2 kernel (csrc/fused.hip) gives the forward bit for bit what its four convs give, whole-graph
     and per-module; every tile shape the planner picks (8 x 16 on 160^2 maps, 4 x 40 below), both tiles forced
-    on every block (FCE_C3K2_TILE) and partial edge tiles (224: 56 = 3.5 x 16 = 1.4 x 40).  FCE_FUSE_C3K2=1 forces the fused
+    on every block (FCE_C3K2_TILE), both y store forms forced on every block (FCE_C3K2_YSTORE: buffer stores
+    whose dropped lanes are the partial tiles' outside pixels, or branched global stores) and partial edge tiles
+    (224: 56 = 3.5 x 16 = 1.4 x 40).  FCE_FUSE_C3K2=1 forces the fused
     form, =0 records the convs only; the default records both and the plan keeps the faster (auto), and every
     combination of forms the auto plan can pick is bitwise the same forward."""
     if tile:
         monkeypatch.setenv("FCE_C3K2_TILE", tile)
+    if ystore:
+        monkeypatch.setenv("FCE_C3K2_YSTORE", ystore)
     model = cases.seeded_model(cfg, 0).to(device)
     x = torch.rand(batch, 3, imgsz, imgsz, generator=torch.Generator().manual_seed(9)).half().to(device)
     monkeypatch.setenv("FCE_FUSE_C3K2", "1")
