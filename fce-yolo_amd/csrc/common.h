@@ -125,6 +125,22 @@ __device__ __forceinline__ float fusion_alpha(const float* w, int n, int i) {
 }
 
 // NHWC element offset of pixel (n,y,x) channel c in a view
+// A store that every lane of the wave issues (no branch around it): a lane with nothing to write stores to an
+// offset past the buffer resource's end, which the hardware drops. Branched stores are counted as maybe-absent,
+// so the compiler's wait for a load issued before them (the next tile's x prefetch) became vmcnt(0), i.e. a wait
+// for the stores too (vmcnt retires in issue order); unconditional ones let it wait for the load alone.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, int(bytes), 0x00020000);  // gfx9 dword3: raw, range-checked
+}
+__device__ __forceinline__ void store_h4_or_drop(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t byte_off, h4 v) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, int(ok ? byte_off : 0x80000000u), 0, 0);
+}
+
+__device__ __forceinline__ void store_h1_or_drop(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t byte_off, _Float16 v) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), r, int(ok ? byte_off : 0x80000000u), 0, 0);
+}
+
 __host__ __device__ __forceinline__ int64_t nhwc_off(int n, int y, int x, int H, int W, int cstride) {
   return ((int64_t(n) * H + y) * W + x) * cstride;
 }

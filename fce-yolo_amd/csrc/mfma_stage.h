@@ -65,18 +65,6 @@ __device__ __forceinline__ void stage_copy_frags(h8* dst, const h8* src, int ct_
   }
 }
 
-// A store that every lane of the wave issues (no branch around it): a lane with nothing to write stores to an
-// offset past the buffer resource's end, which the hardware drops. Branched stores are counted as maybe-absent,
-// so the compiler's wait for a load issued before them (the next tile's x prefetch) became vmcnt(0), i.e. a wait
-// for the stores too (vmcnt retires in issue order); unconditional ones let it wait for the load alone.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, int(bytes), 0x00020000);  // gfx9 dword3: raw, range-checked
-}
-__device__ __forceinline__ void store_h4_or_drop(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t byte_off, h4 v) {
-  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, int(ok ? byte_off : 0x80000000u), 0, 0);
-}
-
 // dense_geom's per-cout-tile fragment count of a (cin, k x k) conv
 inline int stage_nalloc(int cin, int k) {
   const int nsteps = (k * k * (cin / 8) + 3) / 4;
