@@ -147,8 +147,11 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_fused_kernel(Stem2Args a) {
     for (int j = 0; j < 4; ++j) bz1[ct][j] = a.b1[ct * 16 + grp * 4 + j];
   }
   const int fps = (a.Ws + 15) / 16, fpo = (a.Wo + 15) / 16;
+  constexpr int FMAX = (SR2 * 10 + NW - 1) / NW;  // second-conv fragments per wave (st_launch checks fpo <= 10)
   for (int g = g_begin; g < g_end; ++g) {
     const int n = g / rows, oy0 = (g - n * rows) * SR2;
+    const uint32_t yimg = uint32_t(a.Ho) * uint32_t(a.Wo) * uint32_t(a.ycs);
+    const __amdgpu_buffer_rsrc_t yr = out_rsrc(a.y + int64_t(n) * yimg, yimg * 2u);
     const int sy0 = 2 * oy0 - 1;  // first stem row
     // ---------------- input rows (prefetched) -> LDS, the next group's in flight
 #pragma unroll
@@ -199,46 +202,52 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_fused_kernel(Stem2Args a) {
     }
     stage_barrier();
     // ---------------- the second conv from S -> y
-    for (int f = wave; f < SR2 * fpo; f += NW) {
+    // A static FMAX fragments per wave (W <= 640: at most 10 per output row), every one issuing its stores (dropped
+    // past the map / for a wave's spare fragment): with a runtime trip count the stores were maybe-absent to hipcc's
+    // waitcnt pass, and the next group's wait for its input prefetch (issued before them) also waited for them.
+#pragma unroll
+    for (int i = 0; i < FMAX; ++i) {
+      const int f = wave + NW * i;
       const int r1 = f / fpo, fx = f - r1 * fpo;
       const int oy = oy0 + r1;
-      if (oy >= a.Ho) break;  // wave-uniform: f grows with r1
+      const bool wv = f < SR2 * fpo && oy < a.Ho;  // wave-uniform
       const int ox = fx * 16 + col, oxc = min(ox, a.Wo - 1);
       f4 acc[G::CT1];
 #pragma unroll
       for (int ct = 0; ct < G::CT1; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
+      if (wv) {
 #pragma unroll
-      for (int st = 0; st < G::NS1; ++st) {
-        int tap, cc;
-        bool ok;
-        if (G::CM) {  // chunk-major: step = (32-channel chunk) * 9 + tap
-          tap = st % 9;
-          cc = (st / 9) * 4 + grp;
-          ok = true;
-        } else {  // tap-major 8-channel chunk c = 4 st + grp
-          const int c = st * 4 + grp;
-          tap = c / G::K1;
-          cc = c - tap * G::K1;
-          ok = c < 9 * G::K1;
-        }
-        h8 b = h8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (ok) {
-          const int ky = tap / 3, kx = tap - ky * 3;
-          const int cp = 2 * oxc + kx, p = (cp & 1) ? half + (cp >> 1) : (cp >> 1);
-          b = S[((2 * r1 + ky) * npos + p) * G::sS + cc];
-        }
+        for (int st = 0; st < G::NS1; ++st) {
+          int tap, cc;
+          bool ok;
+          if (G::CM) {  // chunk-major: step = (32-channel chunk) * 9 + tap
+            tap = st % 9;
+            cc = (st / 9) * 4 + grp;
+            ok = true;
+          } else {  // tap-major 8-channel chunk c = 4 st + grp
+            const int c = st * 4 + grp;
+            tap = c / G::K1;
+            cc = c - tap * G::K1;
+            ok = c < 9 * G::K1;
+          }
+          h8 b = h8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (ok) {
+            const int ky = tap / 3, kx = tap - ky * 3;
+            const int cp = 2 * oxc + kx, p = (cp & 1) ? half + (cp >> 1) : (cp >> 1);
+            b = S[((2 * r1 + ky) * npos + p) * G::sS + cc];
+          }
 #pragma unroll
-        for (int ct = 0; ct < G::CT1; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[ct][st], b, acc[ct], 0, 0, 0);
+          for (int ct = 0; ct < G::CT1; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[ct][st], b, acc[ct], 0, 0, 0);
+        }
       }
-      if (ox < a.Wo) {
-        _Float16* yo = a.y + nhwc_off(n, oy, ox, a.Ho, a.Wo, a.ycs);
+      const bool ok = wv && ox < a.Wo;
+      const uint32_t off = uint32_t((oy * a.Wo + ox) * a.ycs + grp * 4) * 2u;
 #pragma unroll
-        for (int ct = 0; ct < G::CT1; ++ct) {
-          float v[4];
+      for (int ct = 0; ct < G::CT1; ++ct) {
+        float v[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = silu(acc[ct][j] + bz1[ct][j]);
-          *reinterpret_cast<h4*>(yo + ct * 16 + grp * 4) = h4_of(v);
-        }
+        for (int j = 0; j < 4; ++j) v[j] = silu(acc[ct][j] + bz1[ct][j]);
+        store_h4_or_drop(yr, ok, off + uint32_t(ct * 32), h4_of(v));
       }
     }
     stage_barrier();  // the second conv's reads of S and the stem's of IN before the next group overwrites them
@@ -269,6 +278,7 @@ static int st_launch(const Stem2Args& a, hipStream_t s) {
   constexpr int NXE_MAX = (3 * G::IR * (640 + 16) / 8 + NW * 64 - 1) / (NW * 64);  // register image sized for W <= 640
   const int ne = 3 * G::IR * (a.W + 16) / 8;
   FCE_CHECK(ne <= NXE_MAX * NW * 64, "stem fused: input wider than the prefetch register image (W <= 640)");
+  FCE_CHECK((a.Wo + 15) / 16 <= 10, "stem fused: output wider than the per-wave fragment count (W <= 640)");
   const size_t lds = size_t(3) * G::IR * (a.W + 16) * sizeof(_Float16) + size_t(G::NS) * (a.Ws + 2) * G::sS * 16;
   FCE_CHECK(lds <= 160 * 1024, "stem fused: input too wide for the LDS tile");
   auto k = stem_fused_kernel<T, C0, C1, SR2, NW, NXE_MAX>;
