@@ -233,9 +233,9 @@ class ShardedPredictor:
     def results(self, k: int):
         """(dets, keep) per image of the whole global batch, in the unsharded order (with gather=False: this
         rank's shard only)."""
-        if k == self.pipe.pending:
+        if k == self.pipe.pending or k in self.pipe._group:  # Pipeline.results' condition: post the slot's group
             self.pipe.flush()
-        self.pipe._posted[k].wait()
+        self.pipe.check_posted(k)
         self.pipe.nms_done[k].synchronize()
         if self.do_gather:
             k0, m = self.pipe.group_of(k)
@@ -246,8 +246,7 @@ class ShardedPredictor:
         return [nms.dets[i, : cnt[i]] for i in range(self.batch)], [nms.keep[i, : cnt[i]] for i in range(self.batch)]
 
     def close(self):
-        self.pipe.flush()
-        self.pipe.close()
+        self.pipe.close()  # flushes, then stops the poster
         torch.cuda.synchronize(self.engine.device)
         for e in self.pipe.engs:
             e.close()

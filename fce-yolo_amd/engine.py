@@ -404,6 +404,9 @@ class Pipeline:
         if not ks:
             return
         k0, m = ks[0] - ks[0] % self.G, self.G
+        # groups are aligned slot blocks: a group is posted when its block's last slot is submitted, a flushed partial
+        # group leaves the rest of its block to the next post of the same block, so no group crosses a block boundary
+        assert all(k0 <= k < k0 + m for k in ks), f"post group {ks} crosses the slot block [{k0}, {k0 + m})"
         block = range(k0, k0 + m)
         done = torch.cuda.Event()
         for k in block:
@@ -444,7 +447,7 @@ class Pipeline:
             self.fwd_done[k].record(s)
             if self.used[k] and self.post is not None:
                 # the post of the slot's previous batch has read nms[k] (pred / best are the lane's own: stream order)
-                self._posted[k].wait()
+                self.check_posted(k)
                 if self._wait_always or not self.nms_done[k].query():
                     s.wait_event(self.nms_done[k])
             if not self._skip_nms:
@@ -454,7 +457,7 @@ class Pipeline:
             self.nms_done[k] = self.lane_done[k]
         else:
             self._group.append(k)
-            if len(self._group) == self.G:
+            if k % self.G == self.G - 1:  # the last slot of its block (after a flushed partial group, the rest of it)
                 self._post_group()
         self.used[k] = True
         return k
@@ -492,9 +495,27 @@ class Pipeline:
         if self.poster is not None:
             self.poster.drain()
 
-    def close(self):
+    def check_posted(self, k: int):
+        """Wait until slot k's post has been issued, and raise if a post failed (its outputs would be stale)."""
+        self._posted[k].wait()
         if self.poster is not None:
-            self.poster.close()
+            self.poster._check()
+
+    def close(self):
+        """Issue what is still pending, then stop the poster thread.  A Pipeline with a `post` and lanes runs a host
+        thread (Poster): close it (or use it as a context manager) when done."""
+        try:
+            self.flush()
+        finally:
+            if self.poster is not None:
+                self.poster.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def group_of(self, k: int):
         """(first slot, slots) of the post group slot k was posted with (lanes with post)."""
@@ -507,12 +528,12 @@ class Pipeline:
         main = torch.cuda.current_stream(self.eng.device)
         for j in range(self.depth) if k is None else (k,):
             if self.used[j]:
-                self._posted[j].wait()
+                self.check_posted(j)
                 main.wait_event(self.nms_done[j])
 
     def results(self, k: int):
         if k == self.pending or k in self._group:
             self.flush()
-        self._posted[k].wait()
+        self.check_posted(k)
         self.nms_done[k].synchronize()
         return self.nms[k].results()

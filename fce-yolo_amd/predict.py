@@ -321,6 +321,8 @@ class Predictor:
 
     def _collect(self, ln: _Lane):
         ln.posted.wait()
+        if self.poster is not None:
+            self.poster._check()  # a failed gather / D2H never records ln.done: out_host would hold an older batch
         ln.done.synchronize()
         if self.gather is not None:
             ln.ticket = None

@@ -452,6 +452,47 @@ def test_fused_stem_kept_out_where_it_does_not_fit(device, monkeypatch):
     assert torch.equal(y, y0)
 
 
+def test_fused_stem_locked_when_another_layer_reads_the_stem(device, monkeypatch):
+    """The fused stem pair skips writing the stem's output, so the plan locks it out when any op other than the second
+    conv reads that output: here layer 2 is a second conv from layer 0 (a saved layer), concatenated with layer 1.
+    Even FCE_FUSE_STEM=1 keeps the two convs, and the forward equals the one planned without the alternative."""
+    from fce_yolo_amd.parser import DetectionModel
+    from fce_yolo_amd.weights import seeded_state_dict
+
+    d = {"nc": 80, "scales": {"n": [0.50, 0.25, 1024]}, "scale": "n",
+         "backbone": [[-1, 1, "Conv", [64, 3, 2]], [-1, 1, "Conv", [128, 3, 2]], [0, 1, "Conv", [128, 3, 2]],
+                      [[1, 2], 1, "Concat", [1]], [-1, 1, "Conv", [256, 3, 2]], [-1, 1, "Conv", [512, 3, 2]],
+                      [-1, 1, "Conv", [1024, 3, 2]]],
+         "head": [[[4, 5, 6], 1, "Detect", ["nc"]]]}
+    model = DetectionModel(d)
+    assert 0 in model.save
+    model.load_state_dict(seeded_state_dict([(k, v.shape) for k, v in model.state_dict().items()], 0))
+    model = model.eval().to(device)
+    x = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(6)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_STEM", "1")
+    # the lowering does not record the alternative when layer 0 is saved (modules.stem_alt) ...
+    eng = Engine(model, 1, 256, device)
+    assert "stem_fused" not in [eng.op_info(i)[0] for i in range(eng.num_ops())]
+    y1 = eng(x).clone()
+    # ... and if it were recorded, the plan-time access check (fce_net_plan) locks it out
+    from fce_yolo_amd import modules as M
+
+    real = M.stem_alt
+    monkeypatch.setattr(M, "stem_alt", lambda be, m0, m1, first, saved: real(be, m0, m1, first, False))
+    eng = Engine(model, 1, 256, device)
+    names = [eng.op_info(i)[0] for i in range(eng.num_ops())]
+    assert names.count("stem_fused") == 1
+    i = names.index("stem_fused")
+    assert eng.alt_form(i) == 0 and not eng.skipped(0) and not eng.skipped(1) and eng.skipped(i)
+    with pytest.raises(RuntimeError, match="cannot run"):
+        eng.set_alt_form(i, True)
+    y = eng(x).clone()
+    monkeypatch.setenv("FCE_FUSE_STEM", "0")
+    y0 = Engine(model, 1, 256, device)(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0) and torch.equal(y1, y0)
+
+
 def test_fused_detect_cls_unknown_tile_is_an_error(device, monkeypatch):
     """FCE_DCLS_TILE_64 / _128 name a tile of that instantiation; anything else fails loudly."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)

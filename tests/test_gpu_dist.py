@@ -118,19 +118,46 @@ def _worker_resident(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _worker_midflush(rank, world, port, q):
+    """dist.ShardedPredictor with lanes 3 (post groups of 3 aligned slot blocks, depth 6) and results read MID-STREAM:
+    after batches 1 and 4 every batch submitted so far is read (results() flushes a partial group), then more batches
+    are submitted into the rest of the flushed block; every batch's results are checked (a flushed partial
+    group used to shift later groups across block boundaries, so some slots were never gathered)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fce_yolo_amd.dist import ShardedPredictor
+
+        torch.cuda.set_device(0)
+        sp = ShardedPredictor(_model(), TOTAL, S, "cuda:0", batch_size=BS, lanes=3, gather=True, conf=0.05)
+        assert sp.G == 3 and sp.pipe.depth == 6
+        xs = _resident_inputs(9)
+        out, unread = [None] * len(xs), []
+        for j, x in enumerate(xs):
+            unread.append((j, sp.submit(x[sp.start:sp.end].half().to("cuda:0"))))
+            if j in (1, 4) or j == len(xs) - 1:
+                if j == len(xs) - 1:
+                    sp.flush()
+                for jj, k in unread:
+                    ds, ks = sp.results(k)
+                    out[jj] = ([d.cpu().numpy() for d in ds], [kk.cpu().numpy() for kk in ks])
+                unread = []
+        q.put((rank, out))
+        sp.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def _resident_inputs(nb=5):
     g = torch.Generator().manual_seed(21)
     return [torch.rand(TOTAL, 3, S, S, generator=g) for _ in range(nb)]
 
 
-def test_sharded_predictor_grouped_gather_two_ranks_match_one_engine():
-    """Every rank gets every image's detections, bit-equal to one executor + NMS over the whole batch of 7."""
-    from fce_yolo_amd.engine import NMS, Engine
-
+def _run_ranks(worker):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_resident, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     import queue
@@ -147,31 +174,51 @@ def test_sharded_predictor_grouped_gather_two_ranks_match_one_engine():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
+    return res
+
+
+def _reference(model, xs, bounds):
+    """per batch, per image (dets, keep) from one executor per [lo, hi) range of the batch"""
+    from fce_yolo_amd.engine import NMS, Engine
+
+    out = [([], []) for _ in xs]
+    for lo, hi in bounds:
+        eng = Engine(model, hi - lo, S, "cuda:0")
+        nms = NMS(hi - lo, eng.anchors, eng.nc, "cuda:0", conf=0.05)
+        for j, x in enumerate(xs):
+            dets, keep, counts = nms(eng(x[lo:hi].half().to("cuda:0")).clone())
+            c = counts.tolist()
+            out[j][0].extend(dets[i, :c[i]].cpu().numpy() for i in range(hi - lo))
+            out[j][1].extend(keep[i, :c[i]].cpu().numpy() for i in range(hi - lo))
+        eng.close()
+    return out
+
+
+def _diff(out, want):
+    return [(j, i) for j, ((ds, ks), (wd, wk)) in enumerate(zip(out, want)) for i, (d, k, d1, k1) in
+            enumerate(zip(ds, ks, wd, wk)) if not (np.array_equal(k, k1) and np.array_equal(d, d1))]
+
+
+def test_sharded_predictor_grouped_gather_two_ranks_match_one_engine():
+    """Every rank gets every image's detections, bit-equal to one executor + NMS over the whole batch of 7."""
+    res = _run_ranks(_worker_resident)
     model = _model()
     xs = _resident_inputs()
-
-    def reference(bounds):
-        """per batch, per image (dets, keep) from one executor per [lo, hi) range of the batch"""
-        out = [([], []) for _ in xs]
-        for lo, hi in bounds:
-            eng = Engine(model, hi - lo, S, "cuda:0")
-            nms = NMS(hi - lo, eng.anchors, eng.nc, "cuda:0", conf=0.05)
-            for j, x in enumerate(xs):
-                dets, keep, counts = nms(eng(x[lo:hi].half().to("cuda:0")).clone())
-                c = counts.tolist()
-                out[j][0].extend(dets[i, :c[i]].cpu().numpy() for i in range(hi - lo))
-                out[j][1].extend(keep[i, :c[i]].cpu().numpy() for i in range(hi - lo))
-            eng.close()
-        return out[-len(res[0][1]):]
-
-    def diff(out, want):
-        return [(j, i) for j, ((ds, ks), (wd, wk)) in enumerate(zip(out, want)) for i, (d, k, d1, k1) in
-                enumerate(zip(ds, ks, wd, wk)) if not (np.array_equal(k, k1) and np.array_equal(d, d1))]
-
-    per_shard = reference([(0, BS), (BS, TOTAL)])  # the shards' own executors: what the gather must deliver
+    per_shard = _reference(model, xs, [(0, BS), (BS, TOTAL)])[-len(res[0][1]):]  # what the gather must deliver
     assert sum(len(d) for ds, _ in per_shard for d in ds) > 0
     for rank, out in res:
         assert len(out) == len(per_shard) and all(len(ds) == TOTAL for ds, _ in out)
-        assert not diff(out, per_shard), (rank, diff(out, per_shard))
-    whole = reference([(0, TOTAL)])  # one executor over all 7 images (batch invariance of the forward)
-    assert not diff(res[0][1], whole), diff(res[0][1], whole)
+        assert not _diff(out, per_shard), (rank, _diff(out, per_shard))
+    whole = _reference(model, xs, [(0, TOTAL)])[-len(res[0][1]):]  # one executor over all 7 images
+    assert not _diff(res[0][1], whole), _diff(res[0][1], whole)
+
+
+def test_sharded_predictor_results_mid_stream_two_ranks():
+    """Results read mid-stream (partial post groups flushed, then more batches into the same slot blocks): every one of
+    the nine batches bit-equal to the shards' own executors, on both ranks."""
+    res = _run_ranks(_worker_midflush)
+    per_shard = _reference(_model(), _resident_inputs(9), [(0, BS), (BS, TOTAL)])
+    assert sum(len(d) for ds, _ in per_shard for d in ds) > 0
+    for rank, out in res:
+        assert len(out) == len(per_shard) and all(o is not None and len(o[0]) == TOTAL for o in out)
+        assert not _diff(out, per_shard), (rank, _diff(out, per_shard))
