@@ -113,6 +113,18 @@ class Stem2Desc(C.Structure):
     ]
 
 
+class BneckDesc(C.Structure):
+    """fce_bneck_desc: a chain of n Bottlenecks (w / b: cv1, cv2 of each, in chain order)."""
+    _fields_ = [
+        ("c", C.c_int),
+        ("c_mid", C.c_int),
+        ("n", C.c_int),
+        ("shortcut", C.c_int),
+        ("w", C.c_void_p * 4),
+        ("b", C.c_void_p * 4),
+    ]
+
+
 class NmsOpts(C.Structure):
     """fce_nms_opts: the non-default arguments of non_max_suppression (utils/nms.py:13-29)."""
     _fields_ = [
@@ -137,6 +149,7 @@ _PCO = C.POINTER(CoordDesc)
 _PC3 = C.POINTER(C3k2Desc)
 _PDC = C.POINTER(DclsDesc)
 _PST = C.POINTER(Stem2Desc)
+_PBN = C.POINTER(BneckDesc)
 
 _SIGS = {
     "fce_last_error": (C.c_char_p, []),
@@ -169,6 +182,9 @@ _SIGS = {
     "fce_stem_fused": (_I, [_PST, _PT, _PT, _P]),
     "fce_net_add_stem_alt": (_I, [_P, _PST, _I, _I]),
     "fce_net_set_alt_form": (_I, [_P, _I, _I]),
+    "fce_bneck_supported": (_I, [_PBN]),
+    "fce_bneck_fused": (_I, [_PBN, _PT, _PT, _P]),
+    "fce_net_add_bneck_alt": (_I, [_P, _PBN, _I, _I, _I, _I, _I, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

@@ -285,6 +285,11 @@ class NetBackend:
         autotune keeps the faster form (fce_net_add_c3k2_alt)."""
         N.call("fce_net_add_c3k2_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
 
+    def bneck_alt(self, desc: N.BneckDesc, x: View, y: View, first_op: int, nops: int):
+        """The fused Bottleneck chain as the alternative of ops [first_op, first_op + nops) (its 3x3 convs): the plan keeps
+        the faster form, or the convs where no instantiation covers the map width (fce_net_add_bneck_alt)."""
+        N.call("fce_net_add_bneck_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
+
     def stem_alt(self, desc: N.Stem2Desc, first_op: int, nops: int):
         """The one-kernel stem pair as the alternative of ops [first_op, first_op + nops) (the stem and the second conv):
         the plan keeps the faster form, or the two convs when anything else reads the stem's output

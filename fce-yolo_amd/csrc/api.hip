@@ -50,6 +50,9 @@ bool stem_fused_ok(const fce_stem2_desc& d);
 bool stem_fused_fits(const fce_stem2_desc& d, int h, int w);
 int stem_fused(const fce_stem2_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_detect_epi& e, hipStream_t s);
+bool bneck_fused_ok(const fce_bneck_desc& d);
+bool bneck_fused_fits(const fce_bneck_desc& d, int h, int w);
+int bneck_fused(const fce_bneck_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
 
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
 int scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* sc, hipStream_t s);
@@ -132,6 +135,11 @@ int fce_detect_cls_supported(const fce_dcls_desc* d) { return d && detect_cls_fu
 int fce_detect_cls(const fce_dcls_desc* d, const fce_tensor* x, const fce_detect_epi* e, void* stream) {
   FCE_CHECK(d && x && e, "fce_detect_cls: null argument");
   FCE_GUARD(return detect_cls_fused(*d, *x, *e, S(stream));)
+}
+int fce_bneck_supported(const fce_bneck_desc* d) { return d && bneck_fused_ok(*d) ? 1 : 0; }
+int fce_bneck_fused(const fce_bneck_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
+  FCE_CHECK(d && x && y, "fce_bneck_fused: null argument");
+  FCE_GUARD(return bneck_fused(*d, *x, *y, S(stream));)
 }
 int fce_stem_fused_supported(const fce_stem2_desc* d) { return d && stem_fused_ok(*d) ? 1 : 0; }
 int fce_stem_fused(const fce_stem2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
@@ -222,7 +230,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS, OP_STEM2 };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS, OP_STEM2, OP_BNECK };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -253,6 +261,7 @@ struct OpDesc {
   fce_c3k2_desc c3k2{};              // OP_C3K2
   fce_dcls_desc dcls{};              // OP_DCLS
   fce_stem2_desc stem2{};            // OP_STEM2
+  fce_bneck_desc bneck{};            // OP_BNECK
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
   int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
   // alternative forms: an OP_C3K2 / OP_DCLS added by fce_net_add_c3k2_alt / fce_net_add_detect_cls_alt computes the
@@ -423,6 +432,10 @@ int run_op_impl(fce_net* net, const OpDesc& op, const fce_tensor& input, float* 
       fce_tensor y = net->view(op.out, op.out_coff, op.stem2.c1);
       return stem_fused(op.stem2, x, y, s);
     }
+    case OP_BNECK: {
+      fce_tensor y = net->view(op.out, op.out_coff, op.bneck.c);
+      return bneck_fused(op.bneck, x, y, s);
+    }
     case OP_DCLS: {
       fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, 1, op.strides[0],
                        net->cur_best};
@@ -503,6 +516,10 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
       break;
     case OP_STEM2:
       a.push_back({op.out, op.out_coff, op.out_coff + op.stem2.c1, true});
+      break;
+    case OP_BNECK:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.bneck.c, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.bneck.c, true});
       break;
     case OP_DCLS:
       a.push_back({op.in, op.in_coff, op.in_coff + op.dcls.c0, false});
@@ -652,6 +669,16 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       *bytes = px * d.c0 * 2 + px * d.nc * 4;
       for (const fce_conv_desc& c : cs) *bytes += double(conv_weight_bytes(c));
       *flops = 2.0 * px * (9.0 * d.c0 + double(d.c0) * d.c3 + 9.0 * d.c3 + double(d.c3) * d.c3 + double(d.c3) * d.nc);
+      break;
+    }
+    case OP_BNECK: {  // one read of x, one write of y, the 2 n convs' weights
+      const fce_bneck_desc& d = op.bneck;
+      *name = "bneck_fused";
+      const double px = N * hw(op.in);
+      const fce_conv_desc c1{d.c, d.c_mid, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+      const fce_conv_desc c2{d.c_mid, d.c, 3, 1, 1, FCE_ACT_SILU, 0, FCE_EPI_STORE, nullptr, 0, 0};
+      *bytes = px * d.c * 2 * 2 + d.n * (double(conv_weight_bytes(c1)) + double(conv_weight_bytes(c2)));
+      *flops = 2.0 * px * d.n * (9.0 * d.c * d.c_mid + 9.0 * d.c_mid * d.c);
       break;
     }
     case OP_C3K2: {  // one read of x, one write of y, the four convs' weights
@@ -898,6 +925,49 @@ int fce_net_set_alt_form(fce_net* net, int i, int fused) {
   return FCE_OK;
 }
 
+int fce_net_add_bneck_alt(fce_net* net, const fce_bneck_desc* d, int in, int in_coff, int out, int out_coff,
+                          int first_op, int nops) {
+  FCE_CHECK(net && d && valid_buf(net, in, false) && valid_buf(net, out, false) && (d->n == 1 || d->n == 2) &&
+                nops == 2 * d->n && first_op >= 0 && first_op + nops == int(net->ops.size()),
+            "fce_net_add_bneck_alt: the alternative must be the last 2 n ops added");
+  FCE_CHECK(bneck_fused_ok(*d), "fce_net_add_bneck_alt: unsupported channel configuration");
+  const OpDesc* o = &net->ops[first_op];
+  for (int j = 0; j < nops; ++j) {
+    const fce_conv_desc& c = o[j].conv;
+    const bool odd = j % 2 == 1;
+    FCE_CHECK(o[j].kind == OP_CONV && !o[j].skip && o[j].alt_first < 0 && o[j].dup < 0 && c.k == 3 && c.stride == 1 &&
+                  c.groups == 1 && c.up == 0 && c.act == FCE_ACT_SILU && c.epilogue == FCE_EPI_STORE &&
+                  c.cin == (odd ? d->c_mid : d->c) && c.cout == (odd ? d->c : d->c_mid) && o[j].w == d->w[j] &&
+                  o[j].b == d->b[j],
+              "fce_net_add_bneck_alt: the ops are not this chain's 3x3 SiLU convs (shapes, weights or epilogues differ)");
+    // chain: conv j reads conv j - 1's whole output (the first reads the input); every odd conv adds its
+    // Bottleneck's input (the input of conv j - 1) as the residual; only the last writes the given output
+    const int src = j == 0 ? in : o[j - 1].out, src_off = j == 0 ? in_coff : o[j - 1].out_coff;
+    FCE_CHECK(o[j].in == src && o[j].in_coff == src_off, "fce_net_add_bneck_alt: the ops must form one chain");
+    if (odd)
+      FCE_CHECK(o[j].res == o[j - 1].in && o[j].res_coff == o[j - 1].in_coff,
+                "fce_net_add_bneck_alt: every second conv must add its Bottleneck's input");
+    else
+      FCE_CHECK(o[j].res < 0, "fce_net_add_bneck_alt: the first conv of a Bottleneck has no residual");
+  }
+  FCE_CHECK(o[nops - 1].out == out && o[nops - 1].out_coff == out_coff,
+            "fce_net_add_bneck_alt: the last conv must write the given output");
+  OpDesc op;
+  op.kind = OP_BNECK;
+  op.bneck = *d;
+  op.in = in;
+  op.in_coff = in_coff;
+  op.in_c = d->c;
+  op.out = out;
+  op.out_coff = out_coff;
+  op.alt_first = first_op;
+  op.alt_n = nops;
+  net->drop_graph();
+  net->ops.push_back(op);
+  set_alt_form(net, net->ops.back(), true);  // fused until the plan-time autotune (or the map width) says otherwise
+  return FCE_OK;
+}
+
 int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, int nops) {
   FCE_CHECK(net && d && nops == 2 && first_op >= 0 && first_op + nops == int(net->ops.size()),
             "fce_net_add_stem_alt: the alternative must be the last two ops added");
@@ -1117,11 +1187,11 @@ static int autotune(fce_net* net) {
     return e && strcmp(e, "1") == 0;
   };
   const bool force_c3k2 = forced("FCE_FUSE_C3K2"), force_dcls = forced("FCE_FUSE_DCLS"),
-             force_stem = forced("FCE_FUSE_STEM");
+             force_stem = forced("FCE_FUSE_STEM"), force_bneck = forced("FCE_FUSE_BNECK");
   for (size_t i = 0; i < net->ops.size() && st == FCE_OK; ++i) {
     OpDesc& op = net->ops[i];
     if (op.alt_first < 0 || op.alt_locked || (op.kind == OP_C3K2 && force_c3k2) || (op.kind == OP_DCLS && force_dcls) ||
-        (op.kind == OP_STEM2 && force_stem))
+        (op.kind == OP_STEM2 && force_stem) || (op.kind == OP_BNECK && force_bneck))
       continue;
     float t[2] = {1e30f, 1e30f};  // [convs, fused]
     for (int form = 0; form < 2 && st == FCE_OK; ++form) {
@@ -1215,6 +1285,14 @@ int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags) {
           if (x.buf == s0.out && x.c0 < s0.out_coff + s0.conv.cout && s0.out_coff < x.c1) op.alt_locked = true;
       }
       if (op.alt_locked) set_alt_form(net, op, false);
+    }
+    // a fused Bottleneck chain runs only where an instantiation covers its map width
+    for (OpDesc& op : net->ops) {
+      if (op.kind != OP_BNECK || op.alt_first < 0) continue;
+      const int sh = net->bufs[op.in].shift;
+      op.alt_locked = !bneck_fused_fits(op.bneck, h >> sh, w >> sh);
+      if (op.alt_locked) set_alt_form(net, op, false);
+      else if (const char* e = getenv("FCE_FUSE_BNECK"); e && strcmp(e, "1") == 0) set_alt_form(net, op, true);
     }
     FCE_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&net->arena), std::max<size_t>(off, 256)));
     FCE_HIP_CHECK(hipMalloc(&net->ws, ws));

@@ -287,6 +287,37 @@ def stem_alt(be, m0, m1, first: int, saved: bool):
         be.stem_alt(d, first, 2)
 
 
+def bneck_alt(be, blocks, x, y, first: int):
+    """Graph backend, after the Bottlenecks `blocks` (a chain: the first reads `x`, each the previous one's output, the
+    last writes `y`) were emitted as ops [first, first + 2 len(blocks)): where every block is a shortcut Bottleneck of
+    3x3 SiLU convs with an instantiated (c, c_mid, n), record the one-kernel chain (csrc/bneck.hip) as their
+    alternative.  FCE_FUSE_BNECK: unset / "auto" -- the plan keeps the faster, "1" -- the fused kernel (where the map
+    width is instantiated), "0" -- the convs only."""
+    import os
+
+    if os.environ.get("FCE_FUSE_BNECK", "auto") == "0" or be.shape_only or not hasattr(be, "bneck_alt"):
+        return
+    n = len(blocks)
+    if n not in (1, 2) or be.num_ops() - first != 2 * n or x.up or x.layout != N.NHWC or x.dtype != N.F16:
+        return
+    c, cm = blocks[0].cv1.conv.in_channels, blocks[0].cv1.conv.out_channels
+    for m in blocks:
+        if type(m) is not Bottleneck or not m.add:
+            return
+        for cv, ci, co in ((m.cv1, c, cm), (m.cv2, cm, c)):
+            k = cv.conv
+            if (k.in_channels, k.out_channels, k.kernel_size[0], k.stride[0], k.groups) != (ci, co, 3, 1, 1) or \
+                    not isinstance(cv.act, nn.SiLU):
+                return
+    d = N.BneckDesc()
+    d.c, d.c_mid, d.n, d.shortcut = c, cm, n, 1
+    for j, cv in enumerate(cv for m in blocks for cv in (m.cv1, m.cv2)):
+        nat = conv_native(cv.conv, getattr(cv, "bn", None), True, be.device)
+        d.w[j], d.b[j] = nat.w.data_ptr(), nat.b.data_ptr()
+    if N.lib().fce_bneck_supported(C.byref(d)):
+        be.bneck_alt(d, x, y, first, 2 * n)
+
+
 class DWConv(Conv):
     """conv.py:185-200."""
 
@@ -357,7 +388,9 @@ class C2f(nn.Module):
         self.cv2 = Conv((2 + n) * self.c, c2, 1)
         self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
 
-    def emit(self, be, x, out=None):
+    def emit(self, be, x, out=None, bneck=True):
+        """`bneck`: record each Bottleneck's one-kernel alternative (bneck_alt; off where the caller records the
+        whole block's)."""
         c, n = self.c, len(self.m)
         buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
         # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: when that
@@ -372,7 +405,10 @@ class C2f(nn.Module):
             self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
         for i, m in enumerate(self.m):
             src = dense if (i == 0 and dense is not None) else buf.slice((1 + i) * c, c)
-            m.emit(be, src, out=buf.slice((2 + i) * c, c))
+            first = be.num_ops() if hasattr(be, "num_ops") else None
+            y = m.emit(be, src, out=buf.slice((2 + i) * c, c))
+            if bneck and first is not None and type(m) is Bottleneck:
+                bneck_alt(be, [m], src, y, first)
         return self.cv2.emit(be, buf, out=out)
 
     def forward(self, x):
@@ -420,13 +456,19 @@ class C3(nn.Module):
                     be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None, dup=(a, c2))
                 else:
                     be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None)
+            first, x0 = (be.num_ops() if hasattr(be, "num_ops") else None), a
             for i, m in enumerate(self.m):
                 a = m.emit(be, a, out=rec.slice(0, c_) if i == len(self.m) - 1 else None)
+            if first is not None:
+                bneck_alt(be, list(self.m), x0, a, first)
             return self.cv3.emit(be, rec.slice(0, c_ + c2), out=out)
         buf = be.alloc(x.n, 2 * c_, x.h, x.w)
         a = self.cv1.emit(be, x) if len(self.m) else self.cv1.emit(be, x, out=buf.slice(0, c_))
+        first, x0 = (be.num_ops() if hasattr(be, "num_ops") else None), a
         for i, m in enumerate(self.m):
             a = m.emit(be, a, out=buf.slice(0, c_) if i == len(self.m) - 1 else None)
+        if first is not None and len(self.m):
+            bneck_alt(be, list(self.m), x0, a, first)
         self.cv2.emit(be, x, out=buf.slice(c_, c_))
         return self.cv3.emit(be, buf, out=out)
 
@@ -497,7 +539,7 @@ class C3k2(C2f):
                 return super().emit(be, x, out)
             # both forms: the four convs, then the fused op as their alternative (the plan keeps the faster)
             first = be.num_ops()
-            y = super().emit(be, x, out)
+            y = super().emit(be, x, out, bneck=False)
             n = be.num_ops() - first
             if n == 4:
                 be.c3k2_alt(d, x, y, first, n)

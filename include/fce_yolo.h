@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FCE_ABI_VERSION 6
+#define FCE_ABI_VERSION 7
 
 /* status codes */
 #define FCE_OK 0
@@ -233,6 +233,20 @@ typedef struct fce_stem2_desc {
 int fce_stem_fused_supported(const fce_stem2_desc* d);
 int fce_stem_fused(const fce_stem2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
 
+/* A chain of n (1 or 2) Bottlenecks with the shortcut (block.py Bottleneck.forward :474-476: x = SiLU(cv2(SiLU(cv1(x))))
+ * + x, cv1 3x3 c -> c_mid, cv2 3x3 c_mid -> c) in one kernel: C3k.m (block.py:1087-1108, n = 2, c_mid = c) and the
+ * Bottleneck of C3k2(c3k = False) (:1064-1084, n = 1).  x, y NHWC f16 views of c channels; the intermediates stay in
+ * LDS.  w / b: the 2 n convs' fce_conv_pack_weights images and BN-folded biases in chain order (cv1, cv2 of the first
+ * Bottleneck, then of the second).  Bitwise equal to the 2 n fce_conv2d calls.  fce_bneck_supported: the instantiated
+ * (c, c_mid, n); fce_bneck_fused also needs an instantiation for the map width (else FCE_ERR_INVALID).  ABI v7. */
+typedef struct fce_bneck_desc {
+  int c, c_mid, n, shortcut;
+  const void* w[4];
+  const float* b[4];
+} fce_bneck_desc;
+int fce_bneck_supported(const fce_bneck_desc* d);
+int fce_bneck_fused(const fce_bneck_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
+
 /* ---------------------------------------------------------------- NMS */
 size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 /* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
@@ -311,6 +325,12 @@ int fce_net_add_detect_cls_alt(fce_net* net, const fce_dcls_desc* d, int in_buf,
  * network input and the stride-2 3x3 conv reading all of its output.  fce_net_plan keeps the two convs when any other
  * op reads the stem's output buffer; otherwise the autotune keeps the faster form (FCE_FUSE_STEM=1: fused).  ABI v6. */
 int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, int nops);
+/* The fused Bottleneck chain (fce_bneck_fused) as an ALTERNATIVE to the nops (= 2 n) conv ops just added: the chain's
+ * 3x3 convs, the first reading (in_buf, in_coff), the last writing (out_buf, out_coff), each odd one adding the input of
+ * its Bottleneck.  fce_net_plan keeps the convs when no instantiation covers the planned map width; otherwise the
+ * autotune keeps the faster form (FCE_FUSE_BNECK=1: fused).  ABI v7. */
+int fce_net_add_bneck_alt(fce_net* net, const fce_bneck_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
+                          int first_op, int nops);
 /* Any alternative op (fused C3k2 or fused Detect cls branch): 1 = the fused form runs, 0 = the ops it replaces run,
  * -1 = op i is not an alternative.  ABI v6. */
 int fce_net_alt_form(const fce_net* net, int i);

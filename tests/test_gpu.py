@@ -435,6 +435,112 @@ def test_fused_stem_bitwise_equal_to_two_convs(cfg, batch, imgsz, dtype, sr, nw,
     assert "stem_fused" not in [el.op_info(k)[0] for k in range(el.num_ops())]
 
 
+@pytest.mark.parametrize("batch,imgsz,nfused", [(2, 640, 5), (1, (608, 640), 5), (3, 320, 3), (1, (320, 640), 5),
+                                                  (2, 256, 0)])
+def test_fused_bneck_bitwise_equal_to_convs(batch, imgsz, nfused, device, monkeypatch):
+    """The one-kernel Bottleneck chain (csrc/bneck.hip: the n scale's C3k pairs L7 / L10 / L24 and the 40^2 neck
+    Bottlenecks L15 / L21) gives the forward bit for bit what its 3x3 convs give: full-width bands at 40 and 20 columns,
+    partial last bands (608: 38 and 19 rows), the maps without an instantiation (320: L10 / L24 at 10^2; 256: all)
+    locked to the convs at plan time even under FCE_FUSE_BNECK=1, and every form the auto plan can pick."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    hw = (imgsz, imgsz) if isinstance(imgsz, int) else imgsz
+    x = torch.rand(batch, 3, *hw, generator=torch.Generator().manual_seed(19)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_BNECK", "1")
+    eng = Engine(model, batch, imgsz, device)
+    alts = [i for i in range(eng.num_ops()) if eng.op_info(i)[0] == "bneck_fused"]
+    assert len(alts) == 5 and sum(eng.alt_form(i) for i in alts) == nfused
+    yf = eng(x).clone()
+    monkeypatch.setenv("FCE_FUSE_BNECK", "0")
+    eng2 = Engine(model, batch, imgsz, device)
+    assert "bneck_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
+    yu = eng2(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(yf, yu)
+    monkeypatch.delenv("FCE_FUSE_BNECK")
+    ea = Engine(model, batch, imgsz, device)
+    alts = [i for i in range(ea.num_ops()) if ea.op_info(i)[0] == "bneck_fused" and ea.alt_form(i) >= 0]
+    assert torch.equal(ea(x).clone(), yu)
+    for fused in (False, True):
+        for i in alts:
+            if fused and nfused < 5:
+                try:
+                    ea.set_alt_form(i, True)
+                except RuntimeError:  # locked: no instantiation for this map width
+                    continue
+            else:
+                ea.set_alt_form(i, fused)
+        assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
+
+
+@pytest.mark.parametrize("c,cm,nb,H,W", [(32, 32, 2, 23, 40), (64, 64, 2, 13, 20), (64, 32, 1, 29, 40),
+                                         (64, 32, 1, 3, 20), (32, 32, 2, 1, 20)])
+def test_fused_bneck_c_abi_views_and_parity(c, cm, nb, H, W, device):
+    """fce_bneck_fused through the C-ABI on channel-slice views (in: c of c + 40 channels at offset 24; out: c of c + 16
+    at offset 8) with partial bands and maps shorter than a band: equal to the 2 nb fce_conv2d calls (each odd one with
+    its Bottleneck's input as the residual) bit for bit, the other output channels untouched, and within the op
+    tolerance of an fp64 torch restatement."""
+    n = 2
+    g = torch.Generator().manual_seed(78)
+    specs = [(c, cm), (cm, c)] * nb
+    ws, bs, descs, packed = [], [], [], []
+    for cin, cout in specs:
+        w = torch.randn(cout, cin, 3, 3, generator=g) * (1.5 / (cin * 9) ** 0.5)
+        b = torch.randn(cout, generator=g) * 0.2
+        d = N.ConvDesc(cin, cout, 3, 1, 1, N.ACT_SILU, 0, N.EPI_STORE, None, 0, 0)
+        ws.append(w), bs.append(b.float().to(device)), descs.append(d), packed.append(M.pack_conv(d, w, device))
+    xbuf = torch.randn(n, H, W, c + 40, generator=g).half().to(device)
+    xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, n, c, H, W, c + 40, 24)
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def run(fused):
+        ybuf = torch.full((n, H, W, c + 16), float("nan"), dtype=torch.float16, device=device)
+        yt = N.Tensor(ybuf.data_ptr(), N.F16, N.NHWC, n, c, H, W, c + 16, 8)
+        if fused:
+            d = N.BneckDesc()
+            d.c, d.c_mid, d.n, d.shortcut = c, cm, nb, 1
+            for j in range(2 * nb):
+                d.w[j], d.b[j] = packed[j].data_ptr(), bs[j].data_ptr()
+            assert N.lib().fce_bneck_supported(C.byref(d)) == 1
+            N.call("fce_bneck_fused", C.byref(d), C.byref(xt), C.byref(yt), stream)
+        else:
+            cur, keep = xt, []
+            for j, (cin, cout) in enumerate(specs):
+                last = j == 2 * nb - 1
+                if last:
+                    ot = yt
+                else:
+                    o = torch.empty(n, H, W, cout, dtype=torch.float16, device=device)
+                    keep.append(o)
+                    ot = N.Tensor(o.data_ptr(), N.F16, N.NHWC, n, cout, H, W, cout, 0)
+                if j % 2 == 0:
+                    inp = cur  # this Bottleneck's input: the residual of its second conv
+                N.call("fce_conv2d", C.byref(descs[j]), C.byref(cur), packed[j].data_ptr(), bs[j].data_ptr(),
+                       C.byref(inp) if j % 2 == 1 else None, C.byref(ot), stream)
+                cur = ot
+        torch.cuda.synchronize()
+        return ybuf.cpu()
+
+    yf, yu = run(True), run(False)
+    assert torch.equal(yf[..., 8:8 + c], yu[..., 8:8 + c])
+    assert torch.isnan(yf[..., :8]).all() and torch.isnan(yf[..., 8 + c:]).all()
+    F = torch.nn.functional
+    t = xbuf[..., 24:24 + c].permute(0, 3, 1, 2).double().cpu()
+    for b in range(nb):
+        h = F.silu(F.conv2d(t, ws[2 * b].double(), bs[2 * b].double().cpu(), padding=1)).half().double()
+        t = (F.silu(F.conv2d(h, ws[2 * b + 1].double(), bs[2 * b + 1].double().cpu(), padding=1)) + t).half().double()
+    err = _rel(yf[..., 8:8 + c].permute(0, 3, 1, 2), t)
+    print(f"OPERR bneck {err:.3e}")
+    assert err <= OP_TOL, err
+    # a map width without an instantiation fails loudly
+    bad = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, n, c, H, 24, c + 40, 24)
+    d = N.BneckDesc()
+    d.c, d.c_mid, d.n, d.shortcut = c, cm, nb, 1
+    for j in range(2 * nb):
+        d.w[j], d.b[j] = packed[j].data_ptr(), bs[j].data_ptr()
+    with pytest.raises(RuntimeError, match="map width"):
+        N.call("fce_bneck_fused", C.byref(d), C.byref(bad), C.byref(bad), stream)
+
+
 def test_fused_stem_kept_out_where_it_does_not_fit(device, monkeypatch):
     """The fused stem pair is built for input widths <= 640: at 704 the plan keeps the two convs (locked: the fused form
     cannot be selected, not even with FCE_FUSE_STEM=1), and the forward equals the one without the alternative."""

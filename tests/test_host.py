@@ -92,7 +92,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(L, s)]
     assert not missing, missing
     assert declared <= set(N.EXPORTED) | {"fce_net_create", "fce_net_destroy"}
-    assert L.fce_abi_version() == 6
+    assert L.fce_abi_version() == 7
 
 
 def test_device_count_without_gpu_is_safe():
@@ -274,7 +274,7 @@ def _lowered(cfg, monkeypatch, **env):
     """A model lowered into a NetBackend on the CPU (ops recorded, never planned or run): [(name, alt_form)]."""
     from fce_yolo_amd.backend import NetBackend
 
-    for k in ("FCE_FUSE_STEM", "FCE_FUSE_DCLS", "FCE_FUSE_C3K2"):
+    for k in ("FCE_FUSE_STEM", "FCE_FUSE_DCLS", "FCE_FUSE_C3K2", "FCE_FUSE_BNECK"):
         if k in env:
             monkeypatch.setenv(k, env[k])
         else:
@@ -306,16 +306,24 @@ def test_lowering_records_the_fused_alternatives(monkeypatch):
     names = [n for n, _ in ops]
     alts = [(i, n) for i, (n, f) in enumerate(ops) if f >= 0]
     assert all(ops[i][1] == 1 for i, _ in alts)
-    assert [n for _, n in alts] == ["stem_fused"] + ["c3k2_fused"] * 3 + ["detect_cls_fused"] * 2
+    assert [n for _, n in alts] == (["stem_fused"] + ["c3k2_fused"] * 2 + ["bneck_fused"] * 3 + ["c3k2_fused"] +
+                                    ["bneck_fused"] * 2 + ["detect_cls_fused"] * 2)
     assert names[:3] == ["conv_stem", "conv3x3_mfma", "stem_fused"]
+    # the Bottleneck chains: C3k pairs (L7, L10, L24: four 3x3s) and the 40^2 neck blocks' single Bottleneck (L15, L21)
+    assert [sum(1 for n in names[i - 4:i] if n == "conv3x3_mfma") for i, n in alts if n == "bneck_fused"] == [4, 4, 2, 2, 4]
     for i, n in alts:
         if n == "detect_cls_fused":
             assert names[i - 5:i] == ["dwconv3x3", "conv1x1_mfma", "dwconv3x3", "conv1x1_mfma", "conv1x1_detect_cls"]
             assert names[i - 6] == "conv1x1_detect_box"
         if n == "c3k2_fused":
             assert names[i - 4:i] == ["conv1x1_mfma", "conv3x3_mfma", "conv3x3_mfma", "conv1x1_mfma"]
-    plain = _lowered("yolo11n-fce.yaml", monkeypatch, FCE_FUSE_STEM="0", FCE_FUSE_DCLS="0", FCE_FUSE_C3K2="0")
+    plain = _lowered("yolo11n-fce.yaml", monkeypatch, FCE_FUSE_STEM="0", FCE_FUSE_DCLS="0", FCE_FUSE_C3K2="0",
+                     FCE_FUSE_BNECK="0")
     assert all(f < 0 for _, f in plain) and len(plain) == len(ops) - len(alts)
+    # without the whole-block C3k2 alternative, the n L2 / L4 / L18 Bottlenecks get the chain kernel's instead (their
+    # (c, c_mid) are not instantiated: 16 / 8, 32 / 16), so only the five chains above remain
+    noc3 = [n for n, f in _lowered("yolo11n-fce.yaml", monkeypatch, FCE_FUSE_C3K2="0") if f >= 0]
+    assert noc3.count("bneck_fused") == 5 and "c3k2_fused" not in noc3
     s_ops = [n for n, f in _lowered("yolo11s-bifpn.yaml", monkeypatch) if f >= 0]
     assert "stem_fused" in s_ops and "detect_cls_fused" not in s_ops
     l_ops = [n for n, f in _lowered("yolo11l-fce.yaml", monkeypatch) if f >= 0]
