@@ -432,10 +432,13 @@ int bneck_fused(const fce_bneck_desc& d, const fce_tensor& x, const fce_tensor& 
     const char* de = getenv("FCE_BNECK_DIAG");
     a.diag = de && atoi(de) != 0;
   }
+  // band heights measured per instantiation (profiles/r06_bneck_probe.txt): L7 8 rows (4: 28.0, 10: 21.8 against 19.7
+  // us), L10 / L24 3 rows (224 bands for 256 CUs; 5: 19.8, 4: 17.8 against 17.4 us), L15 / L21 6 rows (4: 17.5, 8: 14.8
+  // against 13.0 us)
   switch (inst) {
     case 0: return bn_launch<32, 32, 2, 40, 8, 8>(a, x.n, s);
     case 1: return bn_launch<32, 32, 2, 20, 8, 8>(a, x.n, s);
-    case 2: return bn_launch<64, 64, 2, 20, 5, 8>(a, x.n, s);
+    case 2: return bn_launch<64, 64, 2, 20, 3, 8>(a, x.n, s);
     case 3: return bn_launch<64, 32, 1, 40, 6, 8>(a, x.n, s);
     default: return bn_launch<64, 32, 1, 20, 8, 8>(a, x.n, s);
   }
