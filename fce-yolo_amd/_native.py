@@ -125,6 +125,19 @@ class BneckDesc(C.Structure):
     ]
 
 
+class Pw2Desc(C.Structure):
+    """fce_pw2_desc: two chained 1x1 convs (w / b / act: op 1, op 2)."""
+    _fields_ = [
+        ("cin1", C.c_int),
+        ("cout1", C.c_int),
+        ("cin2", C.c_int),
+        ("cout2", C.c_int),
+        ("act", C.c_int * 2),
+        ("w", C.c_void_p * 2),
+        ("b", C.c_void_p * 2),
+    ]
+
+
 class NmsOpts(C.Structure):
     """fce_nms_opts: the non-default arguments of non_max_suppression (utils/nms.py:13-29)."""
     _fields_ = [
@@ -150,6 +163,7 @@ _PC3 = C.POINTER(C3k2Desc)
 _PDC = C.POINTER(DclsDesc)
 _PST = C.POINTER(Stem2Desc)
 _PBN = C.POINTER(BneckDesc)
+_PPW = C.POINTER(Pw2Desc)
 
 _SIGS = {
     "fce_last_error": (C.c_char_p, []),
@@ -185,6 +199,9 @@ _SIGS = {
     "fce_bneck_supported": (_I, [_PBN]),
     "fce_bneck_fused": (_I, [_PBN, _PT, _PT, _P]),
     "fce_net_add_bneck_alt": (_I, [_P, _PBN, _I, _I, _I, _I, _I, _I]),
+    "fce_pw2_supported": (_I, [_PPW]),
+    "fce_pw2": (_I, [_PPW, _PT, _PT, _PT, _I, _PT, _PT, _PT, _PT, _I, _P]),
+    "fce_net_add_pw2_alt": (_I, [_P, _PPW, _I]),
     "fce_bicoordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),
     "fce_coordcrossatt": (_I, [_PCO, _PT, _PT, _P, _SZ, _P]),

@@ -290,6 +290,10 @@ class NetBackend:
         the faster form, or the convs where no instantiation covers the map width (fce_net_add_bneck_alt)."""
         N.call("fce_net_add_bneck_alt", self.net, C.byref(desc), x.buf, x.coff, y.buf, y.coff, first_op, nops)
 
+    def pw2_alt(self, desc: N.Pw2Desc, first_op: int):
+        """The fused 1x1 pair as the alternative of ops first_op, first_op + 1 (fce_net_add_pw2_alt)."""
+        N.call("fce_net_add_pw2_alt", self.net, C.byref(desc), first_op)
+
     def stem_alt(self, desc: N.Stem2Desc, first_op: int, nops: int):
         """The one-kernel stem pair as the alternative of ops [first_op, first_op + nops) (the stem and the second conv):
         the plan keeps the faster form, or the two convs when anything else reads the stem's output

@@ -53,6 +53,10 @@ int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_dete
 bool bneck_fused_ok(const fce_bneck_desc& d);
 bool bneck_fused_fits(const fce_bneck_desc& d, int h, int w);
 int bneck_fused(const fce_bneck_desc& d, const fce_tensor& x, const fce_tensor& y, hipStream_t s);
+bool pw2_fused_ok(const fce_pw2_desc& d);
+int pw2_fused(const fce_pw2_desc& d, const fce_tensor& x1, const fce_tensor* r1, const fce_tensor& h, int h_store,
+              const fce_tensor& x2, const fce_tensor* r2, const fce_tensor& y, const fce_tensor* dup, int dup_lo,
+              hipStream_t s);
 
 int letterbox(const fce_letterbox_img* imgs, int n, uint8_t* dst, int H, int W, int pad, hipStream_t s);
 int scale_boxes(float* dets, const int32_t* counts, int n, int max_det, const fce_box_scale* sc, hipStream_t s);
@@ -140,6 +144,13 @@ int fce_bneck_supported(const fce_bneck_desc* d) { return d && bneck_fused_ok(*d
 int fce_bneck_fused(const fce_bneck_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
   FCE_CHECK(d && x && y, "fce_bneck_fused: null argument");
   FCE_GUARD(return bneck_fused(*d, *x, *y, S(stream));)
+}
+int fce_pw2_supported(const fce_pw2_desc* d) { return d && pw2_fused_ok(*d) ? 1 : 0; }
+int fce_pw2(const fce_pw2_desc* d, const fce_tensor* x1, const fce_tensor* r1, const fce_tensor* h, int h_store,
+            const fce_tensor* x2, const fce_tensor* r2, const fce_tensor* y, const fce_tensor* dup, int dup_lo,
+            void* stream) {
+  FCE_CHECK(d && x1 && h && x2 && y, "fce_pw2: null argument");
+  FCE_GUARD(return pw2_fused(*d, *x1, r1, *h, h_store, *x2, r2, *y, dup, dup_lo, S(stream));)
 }
 int fce_stem_fused_supported(const fce_stem2_desc* d) { return d && stem_fused_ok(*d) ? 1 : 0; }
 int fce_stem_fused(const fce_stem2_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream) {
@@ -230,7 +241,7 @@ int fce_copy(const fce_tensor* src, const fce_tensor* dst, void* stream) {
 // ============================================================================ executor
 namespace {
 
-enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS, OP_STEM2, OP_BNECK };
+enum OpKind { OP_CONV, OP_MAXPOOL, OP_WADD, OP_COORD, OP_PSA, OP_DETECT, OP_CONV_DETECT, OP_C3K2, OP_DCLS, OP_STEM2, OP_BNECK, OP_PW2 };
 
 struct BufDesc {
   int c, shift, dtype;
@@ -262,6 +273,8 @@ struct OpDesc {
   fce_dcls_desc dcls{};              // OP_DCLS
   fce_stem2_desc stem2{};            // OP_STEM2
   fce_bneck_desc bneck{};            // OP_BNECK
+  fce_pw2_desc pw2{};                // OP_PW2: op 1 = in / res / out (h), op 2 = in2 / res2 / out2 / dup
+  int in2 = -1, in2_coff = 0, res2 = -1, res2_coff = 0, out2 = -1, out2_coff = 0, h_store = 1;
   int tile = -1;                     // dense conv register tile (autotuned at plan), -1 = heuristic
   int dup = -1, dup_lo = 0, dup_c = 0;  // OP_CONV duplicate store of out channels [dup_lo, +dup_c) into buffer dup
   // alternative forms: an OP_C3K2 / OP_DCLS added by fce_net_add_c3k2_alt / fce_net_add_detect_cls_alt computes the
@@ -436,6 +449,18 @@ int run_op_impl(fce_net* net, const OpDesc& op, const fce_tensor& input, float* 
       fce_tensor y = net->view(op.out, op.out_coff, op.bneck.c);
       return bneck_fused(op.bneck, x, y, s);
     }
+    case OP_PW2: {
+      const fce_pw2_desc& d = op.pw2;
+      const fce_tensor h = net->view(op.out, op.out_coff, d.cout1);
+      const fce_tensor x2 = net->view(op.in2, op.in2_coff, d.cin2);
+      const fce_tensor y = net->view(op.out2, op.out2_coff, d.cout2);
+      fce_tensor r1{}, r2{}, dv{};
+      if (op.res >= 0) r1 = net->view(op.res, op.res_coff, d.cout1);
+      if (op.res2 >= 0) r2 = net->view(op.res2, op.res2_coff, d.cout2);
+      if (op.dup >= 0) dv = net->view(op.dup, 0, op.dup_c);
+      return pw2_fused(d, x, op.res >= 0 ? &r1 : nullptr, h, op.h_store, x2, op.res2 >= 0 ? &r2 : nullptr, y,
+                       op.dup >= 0 ? &dv : nullptr, op.dup_lo, s);
+    }
     case OP_DCLS: {
       fce_detect_epi e{pred, net->anchors, net->level_off[op.level], op.nc, op.reg_max, 1, op.strides[0],
                        net->cur_best};
@@ -520,6 +545,15 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
     case OP_BNECK:
       a.push_back({op.in, op.in_coff, op.in_coff + op.bneck.c, false});
       a.push_back({op.out, op.out_coff, op.out_coff + op.bneck.c, true});
+      break;
+    case OP_PW2:
+      a.push_back({op.in, op.in_coff, op.in_coff + op.pw2.cin1, false});
+      if (op.res >= 0) a.push_back({op.res, op.res_coff, op.res_coff + op.pw2.cout1, false});
+      a.push_back({op.out, op.out_coff, op.out_coff + op.pw2.cout1, true});
+      a.push_back({op.in2, op.in2_coff, op.in2_coff + op.pw2.cin2, false});
+      if (op.res2 >= 0) a.push_back({op.res2, op.res2_coff, op.res2_coff + op.pw2.cout2, false});
+      a.push_back({op.out2, op.out2_coff, op.out2_coff + op.pw2.cout2, true});
+      if (op.dup >= 0) a.push_back({op.dup, 0, op.dup_c, true});
       break;
     case OP_DCLS:
       a.push_back({op.in, op.in_coff, op.in_coff + op.dcls.c0, false});
@@ -669,6 +703,20 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       *bytes = px * d.c0 * 2 + px * d.nc * 4;
       for (const fce_conv_desc& c : cs) *bytes += double(conv_weight_bytes(c));
       *flops = 2.0 * px * (9.0 * d.c0 + double(d.c0) * d.c3 + 9.0 * d.c3 + double(d.c3) * d.c3 + double(d.c3) * d.nc);
+      break;
+    }
+    case OP_PW2: {  // x1, op 2's inputs that are not op 1's output, the residuals, y (+ h when stored), both weights
+      const fce_pw2_desc& d = op.pw2;
+      *name = "pw2_fused";
+      const double px = N * hw(op.in);
+      const fce_conv_desc c1{d.cin1, d.cout1, 1, 1, 1, d.act[0], 0, FCE_EPI_STORE, nullptr, 0, 0};
+      const fce_conv_desc c2{d.cin2, d.cout2, 1, 1, 1, d.act[1], 0, FCE_EPI_STORE, nullptr, 0, 0};
+      const int lo = std::max(op.in2_coff, op.out_coff), hi = std::min(op.in2_coff + d.cin2, op.out_coff + d.cout1);
+      const int over = op.in2 == op.out ? std::max(0, hi - lo) : 0;
+      *bytes = px * 2 * (d.cin1 + (d.cin2 - over) + d.cout2 + (op.h_store ? d.cout1 : 0) + (op.res >= 0 ? d.cout1 : 0) +
+                         (op.res2 >= 0 ? d.cout2 : 0) + (op.dup >= 0 ? op.dup_c : 0)) +
+               double(conv_weight_bytes(c1)) + double(conv_weight_bytes(c2));
+      *flops = 2.0 * px * (double(d.cin1) * d.cout1 + double(d.cin2) * d.cout2);
       break;
     }
     case OP_BNECK: {  // one read of x, one write of y, the 2 n convs' weights
@@ -968,6 +1016,53 @@ int fce_net_add_bneck_alt(fce_net* net, const fce_bneck_desc* d, int in, int in_
   return FCE_OK;
 }
 
+int fce_net_add_pw2_alt(fce_net* net, const fce_pw2_desc* d, int first_op) {
+  FCE_CHECK(net && d && first_op >= 0 && first_op + 2 == int(net->ops.size()),
+            "fce_net_add_pw2_alt: the alternative must be the last two ops added");
+  FCE_CHECK(pw2_fused_ok(*d), "fce_net_add_pw2_alt: unsupported channel configuration");
+  const OpDesc& o1 = net->ops[first_op];
+  const OpDesc& o2 = net->ops[first_op + 1];
+  const int cins[2] = {d->cin1, d->cin2}, couts[2] = {d->cout1, d->cout2};
+  for (int j = 0; j < 2; ++j) {
+    const OpDesc& o = j ? o2 : o1;
+    const fce_conv_desc& c = o.conv;
+    FCE_CHECK(o.kind == OP_CONV && !o.skip && o.alt_first < 0 && o.in >= 0 && c.k == 1 && c.stride == 1 &&
+                  c.groups == 1 && c.up == 0 && c.epilogue == FCE_EPI_STORE && c.act == d->act[j] && c.cin == cins[j] &&
+                  c.cout == couts[j] && o.w == d->w[j] && o.b == d->b[j] && net->bufs[o.out].dtype == FCE_F16 &&
+                  net->bufs[o.in].dtype == FCE_F16 && net->bufs[o.in].shift == net->bufs[o1.in].shift,
+              "fce_net_add_pw2_alt: the two ops are not this pair's 1x1 convs (shapes, weights or epilogues differ)");
+  }
+  FCE_CHECK(o1.dup < 0, "fce_net_add_pw2_alt: op 1 has a duplicate store");
+  const int lo = std::max(o2.in_coff, o1.out_coff), hi = std::min(o2.in_coff + d->cin2, o1.out_coff + d->cout1);
+  FCE_CHECK(o2.in == o1.out && hi > lo, "fce_net_add_pw2_alt: op 2 must read channels of op 1's output buffer");
+  OpDesc op;
+  op.kind = OP_PW2;
+  op.pw2 = *d;
+  op.in = o1.in;
+  op.in_coff = o1.in_coff;
+  op.in_c = d->cin1;
+  op.res = o1.res;
+  op.res_coff = o1.res_coff;
+  op.out = o1.out;
+  op.out_coff = o1.out_coff;
+  op.in2 = o2.in;
+  op.in2_coff = o2.in_coff;
+  op.res2 = o2.res;
+  op.res2_coff = o2.res_coff;
+  op.out2 = o2.out;
+  op.out2_coff = o2.out_coff;
+  op.dup = o2.dup;
+  op.dup_lo = o2.dup_lo;
+  op.dup_c = o2.dup_c;
+  op.h_store = 1;  // fce_net_plan clears it when nothing else reads h
+  op.alt_first = first_op;
+  op.alt_n = 2;
+  net->drop_graph();
+  net->ops.push_back(op);
+  set_alt_form(net, net->ops.back(), true);  // fused until the plan-time autotune says otherwise
+  return FCE_OK;
+}
+
 int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, int nops) {
   FCE_CHECK(net && d && nops == 2 && first_op >= 0 && first_op + nops == int(net->ops.size()),
             "fce_net_add_stem_alt: the alternative must be the last two ops added");
@@ -1187,11 +1282,12 @@ static int autotune(fce_net* net) {
     return e && strcmp(e, "1") == 0;
   };
   const bool force_c3k2 = forced("FCE_FUSE_C3K2"), force_dcls = forced("FCE_FUSE_DCLS"),
-             force_stem = forced("FCE_FUSE_STEM"), force_bneck = forced("FCE_FUSE_BNECK");
+             force_stem = forced("FCE_FUSE_STEM"), force_bneck = forced("FCE_FUSE_BNECK"),
+             force_pw2 = forced("FCE_FUSE_PW2");
   for (size_t i = 0; i < net->ops.size() && st == FCE_OK; ++i) {
     OpDesc& op = net->ops[i];
     if (op.alt_first < 0 || op.alt_locked || (op.kind == OP_C3K2 && force_c3k2) || (op.kind == OP_DCLS && force_dcls) ||
-        (op.kind == OP_STEM2 && force_stem) || (op.kind == OP_BNECK && force_bneck))
+        (op.kind == OP_STEM2 && force_stem) || (op.kind == OP_BNECK && force_bneck) || (op.kind == OP_PW2 && force_pw2))
       continue;
     float t[2] = {1e30f, 1e30f};  // [convs, fused]
     for (int form = 0; form < 2 && st == FCE_OK; ++form) {
@@ -1285,6 +1381,21 @@ int fce_net_plan_ex(fce_net* net, int batch, int h, int w, int flags) {
           if (x.buf == s0.out && x.c0 < s0.out_coff + s0.conv.cout && s0.out_coff < x.c1) op.alt_locked = true;
       }
       if (op.alt_locked) set_alt_form(net, op, false);
+    }
+    // a fused 1x1 pair stores op 1's output only when some other op reads it (the ops of every form count)
+    for (size_t i = 0; i < net->ops.size(); ++i) {
+      OpDesc& op = net->ops[i];
+      if (op.kind != OP_PW2 || op.alt_first < 0) continue;
+      op.h_store = 0;
+      std::vector<Access> acc;
+      for (size_t j = 0; j < net->ops.size() && !op.h_store; ++j) {
+        if (int(j) == op.alt_first || int(j) == op.alt_first + 1 || j == i) continue;
+        OpDesc probe = net->ops[j];
+        probe.skip = false;
+        op_accesses(net, probe, acc);
+        for (const Access& x : acc)
+          if (!x.write && x.buf == op.out && x.c0 < op.out_coff + op.pw2.cout1 && op.out_coff < x.c1) op.h_store = 1;
+      }
     }
     // a fused Bottleneck chain runs only where an instantiation covers its map width
     for (OpDesc& op : net->ops) {

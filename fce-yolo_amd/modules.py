@@ -318,6 +318,32 @@ def bneck_alt(be, blocks, x, y, first: int):
         be.bneck_alt(d, x, y, first, 2 * n)
 
 
+def pw2_alt(be, first: int, nat1, nat2):
+    """Graph backend, after two 1x1 convs were emitted as ops first, first + 1 (the second reading channels of the
+    first's output buffer; nat1 / nat2 their packed _ConvNative): where the channel counts are instantiated, record the
+    one-kernel pair (csrc/pw2.hip) as their alternative.  FCE_FUSE_PW2: unset / "auto" -- the plan keeps the faster,
+    "1" -- the fused kernel, "0" -- the two convs only."""
+    import os
+
+    if os.environ.get("FCE_FUSE_PW2", "auto") == "0" or be.shape_only or not hasattr(be, "pw2_alt"):
+        return
+    if be.num_ops() - first != 2:
+        return
+    d = N.Pw2Desc()
+    d.cin1, d.cout1, d.cin2, d.cout2 = nat1.desc.cin, nat1.desc.cout, nat2.desc.cin, nat2.desc.cout
+    for j, nat in enumerate((nat1, nat2)):
+        if nat.desc.k != 1 or nat.desc.stride != 1 or nat.desc.groups != 1:
+            return
+        d.act[j] = nat.desc.act
+        d.w[j], d.b[j] = nat.w.data_ptr(), nat.b.data_ptr()
+    if N.lib().fce_pw2_supported(C.byref(d)):
+        be.pw2_alt(d, first)
+
+
+def _nat(m: "Conv", device):
+    return conv_native(m.conv, getattr(m, "bn", None), m._act(), device)
+
+
 class DWConv(Conv):
     """conv.py:185-200."""
 
@@ -398,18 +424,25 @@ class C2f(nn.Module):
         # cv1's epilogue (FCE_DUP=1), so the block's 3x3 convs read whole cache lines (n32: 1.5-2.3x the
         # algorithmic bytes are fetched through the slice)
         dense = None
+        k1 = be.num_ops() if hasattr(be, "num_ops") else None
         if getattr(be, "supports_dup", False) and n and c % 8 == 0 and c < 64 and not _no_dup():
             dense = be.alloc(x.n, c, x.h, x.w)
             self.cv1.emit(be, x, out=buf.slice(0, 2 * c), dup=(dense, c))
         else:
             self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
+        if n and isinstance(self.m[0], C3) and dense is None and k1 is not None and not be.shape_only:
+            self.m[0]._pre_pair = (k1, _nat(self.cv1, be.device))  # cv1 -> the C3k's merged cv1 / cv2 (pw2_alt)
         for i, m in enumerate(self.m):
             src = dense if (i == 0 and dense is not None) else buf.slice((1 + i) * c, c)
             first = be.num_ops() if hasattr(be, "num_ops") else None
             y = m.emit(be, src, out=buf.slice((2 + i) * c, c))
             if bneck and first is not None and type(m) is Bottleneck:
                 bneck_alt(be, [m], src, y, first)
-        return self.cv2.emit(be, buf, out=out)
+        k2 = be.num_ops() if hasattr(be, "num_ops") else None
+        y = self.cv2.emit(be, buf, out=out)
+        if n and isinstance(self.m[-1], C3) and k2 is not None and not be.shape_only:
+            pw2_alt(be, k2 - 1, _nat(self.m[-1].cv3, be.device), _nat(self.cv2, be.device))  # C3k cv3 -> cv2
+        return y
 
     def forward(self, x):
         return _run_eager(self, x)
@@ -439,6 +472,7 @@ class C3(nn.Module):
 
     def emit(self, be, x, out=None):
         c_ = self.cv1.conv.out_channels
+        pre = self.__dict__.pop("_pre_pair", None)  # set by an enclosing C3k2 (C2f.emit) for the cv1 -> cv1 / cv2 pair
         if self._cat_ok():
             # rec = [m | b | a]: cv3 reads [m | b] (cat(m(cv1(x)), cv2(x)), block.py:340), and b = cv2(x), a = cv1(x)
             # come from ONE conv over x (x read once, one launch); below 64 channels a dense copy of a is stored too
@@ -456,6 +490,8 @@ class C3(nn.Module):
                     be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None, dup=(a, c2))
                 else:
                     be.conv(nat.desc, xin, y, nat.w.data_ptr(), nat.b.data_ptr(), None)
+                if pre is not None:  # the enclosing C3k2's cv1 was the op before: the pair as one kernel
+                    pw2_alt(be, pre[0], pre[1], nat)
             first, x0 = (be.num_ops() if hasattr(be, "num_ops") else None), a
             for i, m in enumerate(self.m):
                 a = m.emit(be, a, out=rec.slice(0, c_) if i == len(self.m) - 1 else None)
@@ -594,6 +630,9 @@ class Attention(nn.Module):
 
     def emit(self, be, x, out=None, res=None):
         qkv = self.qkv.emit(be, x)
+        pre = self.__dict__.pop("_pre_pair", None)
+        if pre is not None:  # C2PSA's cv1 was the op before: the pair as one kernel
+            pw2_alt(be, pre[0], pre[1], _nat(self.qkv, be.device))
         o = be.alloc(x.n, self.num_heads * self.head_dim, x.h, x.w)
         if not be.shape_only:
             pw, pb = self._pe(be.device)
@@ -615,7 +654,10 @@ class PSABlock(nn.Module):
 
     def emit(self, be, x, out=None):
         x1 = self.attn.emit(be, x, res=x if self.add else None)
+        k = be.num_ops() if hasattr(be, "num_ops") else None
         f = self.ffn[0].emit(be, x1)
+        if k is not None and not be.shape_only:  # attn.proj (+ x) -> ffn[0]
+            pw2_alt(be, k - 1, _nat(self.attn.proj, be.device), _nat(self.ffn[0], be.device))
         return self.ffn[1].emit(be, f, out=out, res=x1 if self.add else None)
 
     def forward(self, x):
@@ -635,11 +677,18 @@ class C2PSA(nn.Module):
 
     def emit(self, be, x, out=None):
         c = self.c
+        k1 = be.num_ops() if hasattr(be, "num_ops") else None
         buf = self.cv1.emit(be, x)  # [a | b]
+        if len(self.m) and k1 is not None and not be.shape_only:
+            self.m[0].attn._pre_pair = (k1, _nat(self.cv1, be.device))  # cv1 -> attn.qkv (pw2_alt)
         b = buf.slice(c, c)
         for i, m in enumerate(self.m):
             b = m.emit(be, b, out=buf.slice(c, c) if i == len(self.m) - 1 else None)
-        return self.cv2.emit(be, buf, out=out)
+        k2 = be.num_ops() if hasattr(be, "num_ops") else None
+        y = self.cv2.emit(be, buf, out=out)
+        if len(self.m) and k2 is not None and not be.shape_only:  # the last ffn[1] (+ x1) -> cv2
+            pw2_alt(be, k2 - 1, _nat(self.m[-1].ffn[1], be.device), _nat(self.cv2, be.device))
+        return y
 
     def forward(self, x):
         return _run_eager(self, x)

@@ -247,6 +247,23 @@ typedef struct fce_bneck_desc {
 int fce_bneck_supported(const fce_bneck_desc* d);
 int fce_bneck_fused(const fce_bneck_desc* d, const fce_tensor* x, const fce_tensor* y, void* stream);
 
+/* Two chained 1x1 stride-1 convs in one kernel: h = act1(W1 x1 + b1) (+ r1) into the view h, then y = act2(W2 x2 +
+ * b2) (+ r2) where x2 is a view of the SAME buffer as h whose channels overlapping h come straight from op 1 (the
+ * pairs of C3k2 / C3k and C2PSA, block.py:303-307, :340, :1455-1464).  h is written to HBM when h_store (another op
+ * reads it).  dup (nullable): op 2's output channels [dup_lo, dup_lo + dup.c) stored a second time (as
+ * fce_conv2d_variant_dup).  act: FCE_ACT_SILU / FCE_ACT_NONE; w / b: the two convs' fce_conv_pack_weights images and
+ * biases.  Bitwise equal to the two fce_conv2d calls.  fce_pw2_supported: the instantiated channel counts.  ABI v7. */
+typedef struct fce_pw2_desc {
+  int cin1, cout1, cin2, cout2;
+  int act[2];
+  const void* w[2];
+  const float* b[2];
+} fce_pw2_desc;
+int fce_pw2_supported(const fce_pw2_desc* d);
+int fce_pw2(const fce_pw2_desc* d, const fce_tensor* x1, const fce_tensor* r1, const fce_tensor* h, int h_store,
+            const fce_tensor* x2, const fce_tensor* r2, const fce_tensor* y, const fce_tensor* dup, int dup_lo,
+            void* stream);
+
 /* ---------------------------------------------------------------- NMS */
 size_t fce_nms_workspace_bytes(int n, int anchors, int max_nms);
 /* pred: (N, 4+nc, A) fp32.  dets: N x max_det x 6 (x1,y1,x2,y2,conf,cls), keep: N x max_det
@@ -331,6 +348,10 @@ int fce_net_add_stem_alt(fce_net* net, const fce_stem2_desc* d, int first_op, in
  * autotune keeps the faster form (FCE_FUSE_BNECK=1: fused).  ABI v7. */
 int fce_net_add_bneck_alt(fce_net* net, const fce_bneck_desc* d, int in_buf, int in_coff, int out_buf, int out_coff,
                           int first_op, int nops);
+/* The fused 1x1 pair (fce_pw2) as an ALTERNATIVE to the two conv ops just added (first_op, first_op + 1: the second
+ * reading channels of the first's output buffer); fce_net_plan decides whether h must still be stored (another op
+ * reads it) and the autotune keeps the faster form (FCE_FUSE_PW2=1: fused).  ABI v7. */
+int fce_net_add_pw2_alt(fce_net* net, const fce_pw2_desc* d, int first_op);
 /* Any alternative op (fused C3k2 or fused Detect cls branch): 1 = the fused form runs, 0 = the ops it replaces run,
  * -1 = op i is not an alternative.  ABI v6. */
 int fce_net_alt_form(const fce_net* net, int i);

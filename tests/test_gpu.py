@@ -541,6 +541,117 @@ def test_fused_bneck_c_abi_views_and_parity(c, cm, nb, H, W, device):
         N.call("fce_bneck_fused", C.byref(d), C.byref(bad), C.byref(bad), stream)
 
 
+@pytest.mark.parametrize("batch,imgsz", [(2, 640), (3, 320), (1, (352, 288))])
+def test_fused_pw2_bitwise_equal_to_convs(batch, imgsz, device, monkeypatch):
+    """The one-kernel 1x1 pair (csrc/pw2.hip: the n scale's C3k2 cv1 -> C3k cv1 / cv2 and C3k cv3 -> cv2 pairs, and
+    C2PSA's cv1 -> qkv, proj (+ b) -> ffn[0], ffn[1] (+ x1) -> cv2) gives the forward bit for bit what the two convs
+    give: partial last pixel tiles (320, 352 x 288), op 1's output stored or not as the plan decides, and every form the
+    auto plan can pick."""
+    model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
+    hw = (imgsz, imgsz) if isinstance(imgsz, int) else imgsz
+    x = torch.rand(batch, 3, *hw, generator=torch.Generator().manual_seed(23)).half().to(device)
+    monkeypatch.setenv("FCE_FUSE_PW2", "1")
+    eng = Engine(model, batch, imgsz, device)
+    alts = [i for i in range(eng.num_ops()) if eng.op_info(i)[0] == "pw2_fused"]
+    assert len(alts) == 9 and all(eng.alt_form(i) == 1 for i in alts)
+    yf = eng(x).clone()
+    monkeypatch.setenv("FCE_FUSE_PW2", "0")
+    eng2 = Engine(model, batch, imgsz, device)
+    assert "pw2_fused" not in [eng2.op_info(i)[0] for i in range(eng2.num_ops())]
+    yu = eng2(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(yf, yu)
+    monkeypatch.delenv("FCE_FUSE_PW2")
+    ea = Engine(model, batch, imgsz, device)
+    alts = [i for i in range(ea.num_ops()) if ea.op_info(i)[0] == "pw2_fused"]
+    assert torch.equal(ea(x).clone(), yu)
+    for fused in (False, True):
+        for i in alts:
+            ea.set_alt_form(i, fused)
+        assert torch.equal(ea(x, graph=True).clone(), yu) and torch.equal(ea(x, graph=False).clone(), yu)
+
+
+@pytest.mark.parametrize("cin1,cout1,cin2,cout2,mode", [(128, 128, 64, 64, "pre"), (64, 64, 192, 128, "post"),
+                                                       (128, 128, 128, 256, "res"), (256, 128, 256, 256, "res_post")])
+def test_fused_pw2_c_abi_views_and_parity(cin1, cout1, cin2, cout2, mode, device):
+    """fce_pw2 through the C-ABI on channel-slice views of a 2 x 17 x 23 map (a partial 64-pixel tile): "pre" -- op 2
+    reads the second half of op 1's output (with a duplicate store of its upper half), "post" -- op 2 reads [E | h] with
+    E from HBM, "res" / "res_post" -- op 1 without activation plus a residual (Attention.proj, ffn[1]); bit for bit the
+    two fce_conv2d calls, the channels outside the views untouched, h stored or not, and within the op tolerance of an
+    fp64 restatement."""
+    n, H, W = 2, 17, 23
+    g = torch.Generator().manual_seed(79)
+    acts = (N.ACT_NONE if mode.startswith("res") else N.ACT_SILU, N.ACT_SILU)
+    ws, bs, descs, packed = [], [], [], []
+    for cin, cout, act in ((cin1, cout1, acts[0]), (cin2, cout2, acts[1])):
+        w = torch.randn(cout, cin, 1, 1, generator=g) * (1.5 / cin ** 0.5)
+        b = torch.randn(cout, generator=g) * 0.2
+        d = N.ConvDesc(cin, cout, 1, 1, 1, act, 0, N.EPI_STORE, None, 0, 0)
+        ws.append(w), bs.append(b.float().to(device)), descs.append(d), packed.append(M.pack_conv(d, w, device))
+    xbuf = torch.randn(n, H, W, cin1 + 32, generator=g).half().to(device)
+    x1 = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, n, cin1, H, W, cin1 + 32, 16)
+    # the shared buffer: h at hoff, op 2's input x2 at x2off (overlapping h)
+    if mode == "pre":
+        width, hoff, x2off = cout1 + 16, 8, 8 + cout1 - cin2
+    elif mode in ("post", "res_post"):
+        width, x2off = cin2 + 24, 16
+        hoff = x2off + cin2 - cout1
+    else:
+        width, hoff, x2off = cout1 + 8, 8, 8
+    rbuf = torch.randn(n, H, W, cout1 + 8, generator=g).half().to(device)
+    r1 = N.Tensor(rbuf.data_ptr(), N.F16, N.NHWC, n, cout1, H, W, cout1 + 8, 8) if mode.startswith("res") else None
+    base = torch.randn(n, H, W, width, generator=g).half().to(device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    dup_c, dup_lo = (cout2 // 2, cout2 // 2) if mode == "pre" else (0, 0)
+
+    def run(fused, h_store):
+        buf = base.clone()
+        ybuf = torch.full((n, H, W, cout2 + 8), float("nan"), dtype=torch.float16, device=device)
+        dbuf = torch.full((n, H, W, max(dup_c, 8)), float("nan"), dtype=torch.float16, device=device)
+        ht = N.Tensor(buf.data_ptr(), N.F16, N.NHWC, n, cout1, H, W, width, hoff)
+        x2 = N.Tensor(buf.data_ptr(), N.F16, N.NHWC, n, cin2, H, W, width, x2off)
+        yt = N.Tensor(ybuf.data_ptr(), N.F16, N.NHWC, n, cout2, H, W, cout2 + 8, 8)
+        dt = N.Tensor(dbuf.data_ptr(), N.F16, N.NHWC, n, dup_c, H, W, max(dup_c, 8), 0) if dup_c else None
+        if fused:
+            d = N.Pw2Desc()
+            d.cin1, d.cout1, d.cin2, d.cout2 = cin1, cout1, cin2, cout2
+            for j in range(2):
+                d.act[j], d.w[j], d.b[j] = acts[j], packed[j].data_ptr(), bs[j].data_ptr()
+            assert N.lib().fce_pw2_supported(C.byref(d)) == 1
+            N.call("fce_pw2", C.byref(d), C.byref(x1), C.byref(r1) if r1 else None, C.byref(ht), int(h_store),
+                   C.byref(x2), None, C.byref(yt), C.byref(dt) if dt else None, dup_lo, stream)
+        else:
+            N.call("fce_conv2d", C.byref(descs[0]), C.byref(x1), packed[0].data_ptr(), bs[0].data_ptr(),
+                   C.byref(r1) if r1 else None, C.byref(ht), stream)
+            if dt:
+                N.call("fce_conv2d_variant_dup", C.byref(descs[1]), C.byref(x2), packed[1].data_ptr(), bs[1].data_ptr(),
+                       None, C.byref(yt), -1, C.byref(dt), dup_lo, stream)
+            else:
+                N.call("fce_conv2d", C.byref(descs[1]), C.byref(x2), packed[1].data_ptr(), bs[1].data_ptr(), None,
+                       C.byref(yt), stream)
+        torch.cuda.synchronize()
+        return buf.cpu(), ybuf.cpu(), dbuf.cpu()
+
+    bu, yu, du = run(False, True)
+    bf, yf, df = run(True, True)
+    assert torch.equal(yf[..., 8:], yu[..., 8:]) and torch.equal(bf, bu)
+    assert not dup_c or torch.equal(df[..., :dup_c], du[..., :dup_c])
+    assert torch.isnan(yf[..., :8]).all()
+    b0, y0, _ = run(True, False)  # h not stored: nothing is written into the shared buffer, y is the same
+    assert torch.equal(y0[..., 8:], yu[..., 8:]) and torch.equal(b0, base.cpu())
+    F = torch.nn.functional
+    t = F.conv2d(xbuf[..., 16:16 + cin1].permute(0, 3, 1, 2).double().cpu(), ws[0].double(), bs[0].double().cpu())
+    t = F.silu(t) if acts[0] == N.ACT_SILU else t
+    if r1:
+        t = t + rbuf[..., 8:8 + cout1].permute(0, 3, 1, 2).double().cpu()
+    hb = base.cpu().permute(0, 3, 1, 2).double().clone()
+    hb[:, hoff:hoff + cout1] = t.half().double()
+    ref = F.silu(F.conv2d(hb[:, x2off:x2off + cin2], ws[1].double(), bs[1].double().cpu()))
+    err = _rel(yf[..., 8:8 + cout2].permute(0, 3, 1, 2), ref)
+    print(f"OPERR pw2 {mode} {err:.3e}")
+    assert err <= OP_TOL, err
+
+
 def test_fused_stem_kept_out_where_it_does_not_fit(device, monkeypatch):
     """The fused stem pair is built for input widths <= 640: at 704 the plan keeps the two convs (locked: the fused form
     cannot be selected, not even with FCE_FUSE_STEM=1), and the forward equals the one without the alternative."""

@@ -274,7 +274,7 @@ def _lowered(cfg, monkeypatch, **env):
     """A model lowered into a NetBackend on the CPU (ops recorded, never planned or run): [(name, alt_form)]."""
     from fce_yolo_amd.backend import NetBackend
 
-    for k in ("FCE_FUSE_STEM", "FCE_FUSE_DCLS", "FCE_FUSE_C3K2", "FCE_FUSE_BNECK"):
+    for k in ("FCE_FUSE_STEM", "FCE_FUSE_DCLS", "FCE_FUSE_C3K2", "FCE_FUSE_BNECK", "FCE_FUSE_PW2"):
         if k in env:
             monkeypatch.setenv(k, env[k])
         else:
@@ -306,11 +306,16 @@ def test_lowering_records_the_fused_alternatives(monkeypatch):
     names = [n for n, _ in ops]
     alts = [(i, n) for i, (n, f) in enumerate(ops) if f >= 0]
     assert all(ops[i][1] == 1 for i, _ in alts)
-    assert [n for _, n in alts] == (["stem_fused"] + ["c3k2_fused"] * 2 + ["bneck_fused"] * 3 + ["c3k2_fused"] +
-                                    ["bneck_fused"] * 2 + ["detect_cls_fused"] * 2)
+    # stem; C3k2 L2, L4; L7 [pair, chain, pair]; L10 [pair, chain, pair]; C2PSA L12 three pairs; chain L15; C3k2 L18;
+    # chain L21; L24 [pair, chain, pair]; Detect cls P3, P4
+    assert [n for _, n in alts] == (["stem_fused"] + ["c3k2_fused"] * 2 + ["pw2_fused", "bneck_fused", "pw2_fused"] * 2 +
+                                    ["pw2_fused"] * 3 + ["bneck_fused", "c3k2_fused", "bneck_fused"] +
+                                    ["pw2_fused", "bneck_fused", "pw2_fused"] + ["detect_cls_fused"] * 2)
     assert names[:3] == ["conv_stem", "conv3x3_mfma", "stem_fused"]
     # the Bottleneck chains: C3k pairs (L7, L10, L24: four 3x3s) and the 40^2 neck blocks' single Bottleneck (L15, L21)
     assert [sum(1 for n in names[i - 4:i] if n == "conv3x3_mfma") for i, n in alts if n == "bneck_fused"] == [4, 4, 2, 2, 4]
+    # every 1x1 pair replaces the two 1x1 convs right before it
+    assert all(names[i - 2:i] == ["conv1x1_mfma"] * 2 for i, n in alts if n == "pw2_fused")
     for i, n in alts:
         if n == "detect_cls_fused":
             assert names[i - 5:i] == ["dwconv3x3", "conv1x1_mfma", "dwconv3x3", "conv1x1_mfma", "conv1x1_detect_cls"]
@@ -318,7 +323,7 @@ def test_lowering_records_the_fused_alternatives(monkeypatch):
         if n == "c3k2_fused":
             assert names[i - 4:i] == ["conv1x1_mfma", "conv3x3_mfma", "conv3x3_mfma", "conv1x1_mfma"]
     plain = _lowered("yolo11n-fce.yaml", monkeypatch, FCE_FUSE_STEM="0", FCE_FUSE_DCLS="0", FCE_FUSE_C3K2="0",
-                     FCE_FUSE_BNECK="0")
+                     FCE_FUSE_BNECK="0", FCE_FUSE_PW2="0")
     assert all(f < 0 for _, f in plain) and len(plain) == len(ops) - len(alts)
     # without the whole-block C3k2 alternative, the n L2 / L4 / L18 Bottlenecks get the chain kernel's instead (their
     # (c, c_mid) are not instantiated: 16 / 8, 32 / 16), so only the five chains above remain
