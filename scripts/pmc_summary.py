@@ -46,7 +46,8 @@ def family(name):
                      ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"), ("pool_kernel", "bicoordcrossatt"),
                      ("pool_band", "bicoordcrossatt"), ("conv3x3_wide", "conv3x3_mfma"),
                      ("coord_", "bicoordcrossatt"), ("gate_apply", "bicoordcrossatt"), ("nms", "nms"),
-                     ("detect_decode", "detect_decode"), ("c3k2_fused", "c3k2_fused")):
+                     ("detect_decode", "detect_decode"), ("c3k2_fused", "c3k2_fused"), ("bneck_fused", "bneck_fused"),
+                     ("pw2_kernel", "pw2_fused")):
         if key in name:
             return fam
     return None
