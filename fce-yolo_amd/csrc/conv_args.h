@@ -432,6 +432,25 @@ static constexpr bool big3_ok(int s, int wm, int ab, int nw = 4) {
   return nw == 4 && (ab == 2 || ab == 3) && (s == 1 ? (wm == 1 || wm == 2) : wm == 2);
 }
 int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hipStream_t s);
+// Persistent 3x3 ring fed by LDS-DMA (conv3x3_dring.hip), coded 0xD00 | rp << 4 | (cpw - 1) << 3 | (nbuf - 2): cin
+// 32 / 64, cpw cout tiles per wave (1: 4 waves along the couts; 2: 2 x 2 waves), rp rows x 16 columns per wave,
+// nbuf LDS tile buffers (nbuf - 1 tiles of input in flight)
+template <int S, int RP, int NCH, int WRW = 1>
+struct Dring3Geom {
+  static constexpr int TW = 16, TH = WRW * RP;  // WRW waves along the rows (2 when each wave owns 2 cout tiles)
+  static constexpr int RI = (TH - 1) * S + 3, CI = (TW - 1) * S + 3;
+  static constexpr int NQ = 4 * NCH, NE = RI * CI * NQ;
+  static constexpr int NINS = (NE + 63) / 64;  // 1 KiB copy instructions per tile
+  static constexpr int DPW = (NINS + 3) / 4;   // per wave (4 waves), padded
+  static constexpr int BUF = DPW * 4 * 64;     // pieces per tile buffer
+};
+
+static constexpr bool dring3_fits(int s, int rp, int nch, int nbuf, int cpw = 1) {
+  return size_t(nbuf) * ((((((cpw * rp - 1) * s + 3) * (15 * s + 3) * 4 * nch + 63) / 64 + 3) / 4) * 4 * 64) * 16 <=
+             80 * 1024 &&       // two blocks per CU
+         (cpw == 1 || nch == 1);  // two cout tiles of 64-channel A fragments spill at two waves per SIMD
+}
+int launch_dring3(const ConvArgs& a, int rp, int nbuf, int cpw, int stride, hipStream_t s);
 // Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
 bool wide3_ok(int stride, int cw);
 int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);

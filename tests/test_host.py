@@ -158,8 +158,8 @@ def test_dw_and_stem_packing():
     (512, 512, 1, 1, {0x400, 0x700, 0xB00}, {0x800}),  # wide 1x1: LDS tile, big-tile pipelined, 256-wide tiles
     (256, 32, 1, 1, {0x400}, {0x700, 0xB00}),       # narrow cout: no 64-cout-per-wave tile
     (48, 128, 1, 1, {0x400}, {0x300, 0x700, 0xB00}),  # cin % 32 != 0: no streaming, cin < 64: no big tile
-    (64, 64, 3, 1, {0x100, 0x600, 0x800, 0xC00}, {0x400, 0x700}),  # 3x3: halo tiles, ring, big tiles, GEMM
-    (256, 256, 3, 2, {0x100, 0x800, 0xC00}, {0x600, 0x700, 0xB00}),  # wide stride-2 3x3: + LDS-DMA tiles, GEMM
+    (64, 64, 3, 1, {0x100, 0x600, 0x800, 0xC00, 0xD00}, {0x400, 0x700}),  # 3x3: halo tiles, rings, big tiles, GEMM
+    (256, 256, 3, 2, {0x100, 0x800, 0xC00}, {0x600, 0x700, 0xB00, 0xD00}),  # wide stride-2 3x3: + LDS-DMA tiles, GEMM
     (256, 96, 3, 2, {0x100, 0xC00}, {0x800}),        # stride 2 needs 128 couts per LDS-DMA big-tile block
     (64, 32, 3, 1, {0x100}, {0xC00}),                # the implicit GEMM needs >= 64 couts
     (16, 32, 3, 2, {0x200}, {0x100, 0x700, 0x800, 0xC00}),  # small-cin 3x3
@@ -172,7 +172,7 @@ def test_conv_variant_enumeration(cin, cout, k, stride, kinds_in, kinds_out):
     nv = N.lib().fce_conv_variants(C.byref(d), 80, codes, 128)
     kinds = {c & 0xF00 for c in codes[:nv]}
     assert nv >= 2 and len(set(codes[:nv])) == nv
-    assert kinds <= {0x000, 0x100, 0x200, 0x300, 0x400, 0x500, 0x600, 0x700, 0x800, 0xA00, 0xB00, 0xC00}
+    assert kinds <= {0x000, 0x100, 0x200, 0x300, 0x400, 0x500, 0x600, 0x700, 0x800, 0xA00, 0xB00, 0xC00, 0xD00}
     assert kinds_in <= kinds and not (kinds_out & kinds)
 
 
