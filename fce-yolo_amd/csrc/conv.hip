@@ -2457,9 +2457,9 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
         if (n < cap) out[n++] = 0x600 | (rp << 4) | (pd - 1);
   if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % 16 == 0 && d.up == 0 && !det_box && !no_ring() && !no_dring())
     for (int cpw : {1, 2})  // persistent LDS-DMA ring: 0xD00 | rp << 4 | (cpw - 1) << 3 | (nbuf - 2)
-      for (int rp : {2, 4})
+      for (int rp : {2, 4, 8})
         for (int nbuf : {3, 4})
-          if (n < cap && d.cout % (16 * cpw) == 0 && dring3_fits(d.stride, rp, d.cin / 32, nbuf, cpw))
+          if (n < cap && d.cout % (16 * cpw) == 0 && (rp < 8 || cpw == 1) && dring3_fits(d.stride, rp, d.cin / 32, nbuf, cpw))
             out[n++] = 0xD00 | (rp << 4) | ((cpw - 1) << 3) | (nbuf - 2);
   if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % 32 == 0 && d.up == 0 && !det_box && !no_ring() &&
       !no_ring32())  // persistent 32x32x16 ring: 0x900 | rpw << 4 | log2(wc) << 12
@@ -2974,7 +2974,8 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
     rp = (tile >> 4) & 15;
     const int nbuf = (tile & 7) + 2, cpw = ((tile >> 3) & 1) + 1;
     FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % (16 * cpw) == 0 && out_kind == OUT_F16 && d.up == 0 &&
-                  (rp == 2 || rp == 4) && (nbuf == 3 || nbuf == 4) && dring3_fits(d.stride, rp, d.cin / 32, nbuf, cpw),
+                  (rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) && (nbuf == 3 || nbuf == 4) &&
+                  dring3_fits(d.stride, rp, d.cin / 32, nbuf, cpw),
               "conv: bad 3x3 LDS-DMA ring hint");
     // the copies and the unconditional stores address input and output through buffer resources (byte offsets < 2^31),
     // the output as 8-byte pieces: other views take the register ring, which gives the same bits

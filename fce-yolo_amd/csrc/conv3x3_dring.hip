@@ -109,25 +109,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
   const int rcs = a.res ? a.rcs : 0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<_Float16*>(a.x), 0, int(uint32_t(a.N) * uint32_t(a.Hs) * uint32_t(a.Ws) * uint32_t(a.xcs) * 2u), 0x00020000);
+  // the copy pieces of this lane, tile-invariant: LDS slot e = (wave + 4 j) * 64 + lane holds piece dr_slot(u, s) of
+  // staged position u = (row r, column c); its element offset from the tile's origin, and r / c for the bounds test
+  // (padding slots past NE get a row that never passes it)
+  int crow[DPW], ccol[DPW], crel[DPW];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int e = (wave + 4 * j) * 64 + lane;
+    const int u = e / NQ, sq = e - u * NQ;
+    const int r = u / CI, cc = u - r * CI;
+    const int c = S == 1 ? cc : (cc < (CI + 1) / 2 ? 2 * cc : 2 * (cc - (CI + 1) / 2) + 1);
+    crow[j] = e < NE ? r : -(1 << 20);
+    ccol[j] = c;
+    crel[j] = (r * a.Ws + c) * a.xcs + dr_slot<KP>(u, sq) * 8;
+  }
   // copies of the k-th tile of this block (clamped to its last: the look-ahead past the end re-copies it) into buffer b
   auto issue = [&](int k, int b) {
     const int tt = tbeg + min(k, count - 1) * step;
     const int tx = tt % tiles_x, r0 = tt / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
     const int iy0 = ty * TH * S - 1, ix0 = tx * TW * S - 1;
-    const int64_t nb = int64_t(n) * a.Hs;
+    const int org = ((n * a.Hs + iy0) * a.Ws + ix0) * a.xcs;  // element offset of the staged origin (< 2^30)
     h8* const dst = dring_smem + b * BUF;
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
-      const int ins = wave + 4 * j, e = ins * 64 + lane;
-      const int u = e / NQ, sq = e - u * NQ;
-      const int r = u / CI, cc = u - r * CI;
-      const int c = S == 1 ? cc : (cc < (CI + 1) / 2 ? 2 * cc : 2 * (cc - (CI + 1) / 2) + 1);
-      const int iy = iy0 + r, ix = ix0 + c;
-      const bool ok = e < NE && iy >= 0 && iy < a.Hs && ix >= 0 && ix < a.Ws;
-      const uint32_t off = uint32_t(((nb + iy) * a.Ws + ix) * a.xcs + dr_slot<KP>(u, sq) * 8) * 2u;
+      const bool ok = unsigned(iy0 + crow[j]) < unsigned(a.Hs) && unsigned(ix0 + ccol[j]) < unsigned(a.Ws);
       // out of the image / padding: an offset past the resource's end, which reads zeros (no branch, no zero line)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (void __attribute__((address_space(3)))*)(dst + ins * 64), 16,
-                                               ok ? off : 0x80000000u, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (void __attribute__((address_space(3)))*)(dst + (wave + 4 * j) * 64),
+                                               16, ok ? uint32_t(org + crel[j]) * 2u : 0x80000000u, 0, 0, 0);
     }
   };
 #pragma unroll
@@ -144,6 +152,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
     const int tt = tbeg + k * step;
     const int tx = tt % tiles_x, r0 = tt / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
     const int oy0 = ty * TH + wr * RP, ox = tx * TW + col;
+    const int pix0 = (n * a.Ho + oy0) * a.Wo + ox;  // output pixel of row p: pix0 + p Wo (< 2^30: the output < 2 GiB)
     // residuals first (clamped, unconditional: the zero line without one), then the copies of tile k + NBUF - 1 into
     // the buffer tile k - 1 used: the epilogue's wait for the residuals leaves those copies in flight
     h4 rres[CPW][RP];
@@ -151,8 +160,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
     for (int cl = 0; cl < CPW; ++cl)
 #pragma unroll
       for (int p = 0; p < RP; ++p) {
-        const int64_t pix = (int64_t(n) * a.Ho + min(oy0 + p, a.Ho - 1)) * a.Wo + min(ox, a.Wo - 1);
-        rres[cl][p] = *reinterpret_cast<const h4*>(rbase + pix * rcs + (a.res ? co0[cl] : 0));
+        const int pix = (n * a.Ho + min(oy0 + p, a.Ho - 1)) * a.Wo + min(ox, a.Wo - 1);
+        rres[cl][p] = *reinterpret_cast<const h4*>(rbase + int64_t(pix) * rcs + (a.res ? co0[cl] : 0));
       }
     issue(k + NBUF - 1, (k + NBUF - 1) % NBUF);
     const h8* const img = dring_smem + (k % NBUF) * BUF;
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
           for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rres[cl][p][j]);
         }
         const bool ok = cok[cl] && oy < a.Ho && ox < a.Wo;
-        const uint32_t off = uint32_t(((int64_t(n) * a.Ho + oy) * a.Wo + ox) * a.ycs + co0[cl]) * 2u;
+        const uint32_t off = uint32_t((pix0 + p * a.Wo) * a.ycs + co0[cl]) * 2u;
         store_h4_or_drop(yr, ok, off, h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])});
       }
   }
@@ -234,8 +243,10 @@ template <int S, int NCH, int CPW>
 static void launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int ntiles, hipStream_t s) {
   if (rp == 2)
     nbuf == 3 ? launch_dring3_k<S, 2, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 2, NCH, 4, CPW>(a, ntiles, s);
-  else
+  else if (rp == 4)
     nbuf == 3 ? launch_dring3_k<S, 4, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 4, NCH, 4, CPW>(a, ntiles, s);
+  else if constexpr (CPW == 1)
+    nbuf == 3 ? launch_dring3_k<S, 8, NCH, 3, 1>(a, ntiles, s) : launch_dring3_k<S, 8, NCH, 4, 1>(a, ntiles, s);
 }
 
 template <int S, int NCH>
@@ -245,7 +256,7 @@ static void launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int nt
 
 // nbuf: tile buffers of the LDS-DMA ring (nbuf - 1 tiles of input in flight ahead of the MFMAs); cpw: cout tiles per wave
 int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int stride, hipStream_t s) {
-  FCE_CHECK((a0.cin == 32 || a0.cin == 64) && a0.cout % (16 * cpw) == 0 && (rp == 2 || rp == 4) &&
+  FCE_CHECK((a0.cin == 32 || a0.cin == 64) && a0.cout % (16 * cpw) == 0 && (rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) &&
                 (nbuf == 3 || nbuf == 4) && (cpw == 1 || cpw == 2) && (stride == 1 || stride == 2) &&
                 dring3_fits(stride, rp, a0.cin / 32, nbuf, cpw),
             "conv 3x3 LDS-DMA ring: bad configuration");

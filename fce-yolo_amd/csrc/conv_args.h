@@ -448,7 +448,8 @@ struct Dring3Geom {
 static constexpr bool dring3_fits(int s, int rp, int nch, int nbuf, int cpw = 1) {
   return size_t(nbuf) * ((((((cpw * rp - 1) * s + 3) * (15 * s + 3) * 4 * nch + 63) / 64 + 3) / 4) * 4 * 64) * 16 <=
              80 * 1024 &&       // two blocks per CU
-         (cpw == 1 || nch == 1);  // two cout tiles of 64-channel A fragments spill at two waves per SIMD
+         (cpw == 1 || nch == 1) &&               // two cout tiles of 64-channel A fragments spill at two waves
+         (rp < 8 || (nch == 1 && nbuf == 3));  // per SIMD, and so do 8-row tiles of them (or with four buffers)
 }
 int launch_dring3(const ConvArgs& a, int rp, int nbuf, int cpw, int stride, hipStream_t s);
 // Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
