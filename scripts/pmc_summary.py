@@ -40,7 +40,7 @@ def family(name):
         out = int(m.group(1))
         return "conv1x1_detect_box" if out == 4 else "conv1x1_detect_cls" if out == 5 else "conv1x1_mfma"
     for key, fam in (("stem_fused", "stem_fused"), ("detect_cls_fused", "detect_cls_fused"),
-                     ("conv3x3_tile", "conv3x3_mfma"), ("conv3x3_ring", "conv3x3_mfma"), ("conv3x3_big", "conv3x3_mfma"),
+                     ("conv3x3_tile", "conv3x3_mfma"), ("conv3x3_ring", "conv3x3_mfma"), ("conv3x3_dring", "conv3x3_mfma"), ("conv3x3_big", "conv3x3_mfma"),
                      ("conv1x1_pipe", "conv1x1_mfma"), ("stem", "conv_stem"), ("psa_attention", "psa_attention"),
                      ("dwconv", "dwconv3x3"), ("maxpool", "maxpool_chain"), ("weighted_add", "bifpn_weighted_add"),
                      ("pool_rows", "bicoordcrossatt"), ("pool_cols", "bicoordcrossatt"), ("pool_kernel", "bicoordcrossatt"),
