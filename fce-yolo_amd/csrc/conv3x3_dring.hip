@@ -220,38 +220,37 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
 }
 
 template <int S, int RP, int NCH, int NBUF, int CPW>
-static void launch_dring3_k(const ConvArgs& a, int ntiles, hipStream_t s) {
+static int launch_dring3_k(const ConvArgs& a, int ntiles, hipStream_t s) {
   if constexpr (!dring3_fits(S, RP, NCH, NBUF, CPW)) {
-    return;  // not a candidate (conv_tile_candidates checks dring3_fits)
+    return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: configuration not instantiated");  // launch_dring3 checks first
   } else {
     constexpr size_t lds = size_t(NBUF) * Dring3Geom<S, RP, NCH, CPW == 1 ? 1 : 2>::BUF * 16;
     auto k = conv3x3_dring_kernel<S, RP, NCH, NBUF, CPW>;
     static const bool big = lds <= 64 * 1024 || hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                      160 * 1024) == hipSuccess;
-    if (!big) {
-      fail(FCE_ERR_HIP, "conv 3x3 LDS-DMA ring: cannot opt in to >64 KiB LDS");
-      return;
-    }
+    if (!big) return fail(FCE_ERR_HIP, "conv 3x3 LDS-DMA ring: cannot opt in to >64 KiB LDS");
     static const int occ = dr_blocks_per_cu(reinterpret_cast<const void*>(k), lds);
     const int nslot = dr_slots(ntiles, a.gy, occ);
     FCE_LAUNCH(k, dim3(unsigned(8 * a.gy * nslot)), dim3(256), lds, s, a, nslot);
+    return launch_status("conv3x3_dring_kernel");
   }
 }
 
 template <int S, int NCH, int CPW>
-static void launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int ntiles, hipStream_t s) {
+static int launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int ntiles, hipStream_t s) {
   if (rp == 2)
-    nbuf == 3 ? launch_dring3_k<S, 2, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 2, NCH, 4, CPW>(a, ntiles, s);
-  else if (rp == 4)
-    nbuf == 3 ? launch_dring3_k<S, 4, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 4, NCH, 4, CPW>(a, ntiles, s);
-  else if constexpr (CPW == 1)
-    nbuf == 3 ? launch_dring3_k<S, 8, NCH, 3, 1>(a, ntiles, s) : launch_dring3_k<S, 8, NCH, 4, 1>(a, ntiles, s);
+    return nbuf == 3 ? launch_dring3_k<S, 2, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 2, NCH, 4, CPW>(a, ntiles, s);
+  if (rp == 4)
+    return nbuf == 3 ? launch_dring3_k<S, 4, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 4, NCH, 4, CPW>(a, ntiles, s);
+  if constexpr (CPW == 1)
+    return nbuf == 3 ? launch_dring3_k<S, 8, NCH, 3, 1>(a, ntiles, s) : launch_dring3_k<S, 8, NCH, 4, 1>(a, ntiles, s);
+  return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: 8-row tiles need one cout tile per wave");
 }
 
 template <int S, int NCH>
-static void launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int ntiles, hipStream_t s) {
-  cpw == 1 ? launch_dring3_s<S, NCH, 1>(a, rp, nbuf, ntiles, s) : launch_dring3_s<S, NCH, 2>(a, rp, nbuf, ntiles, s);
+static int launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int ntiles, hipStream_t s) {
+  return cpw == 1 ? launch_dring3_s<S, NCH, 1>(a, rp, nbuf, ntiles, s) : launch_dring3_s<S, NCH, 2>(a, rp, nbuf, ntiles, s);
 }
 
 // nbuf: tile buffers of the LDS-DMA ring (nbuf - 1 tiles of input in flight ahead of the MFMAs); cpw: cout tiles per wave
@@ -270,10 +269,10 @@ int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int stride, hip
   a.gy = ((a.cout + 15) / 16 + 3) / 4;  // 4 cout tiles per block either way
   const int nch = a.cin / 32;
   if (stride == 1)
-    nch == 1 ? launch_dring3_c<1, 1>(a, rp, nbuf, cpw, int(ntiles), s) : launch_dring3_c<1, 2>(a, rp, nbuf, cpw, int(ntiles), s);
-  else
-    nch == 1 ? launch_dring3_c<2, 1>(a, rp, nbuf, cpw, int(ntiles), s) : launch_dring3_c<2, 2>(a, rp, nbuf, cpw, int(ntiles), s);
-  return launch_status("conv3x3_dring_kernel");
+    return nch == 1 ? launch_dring3_c<1, 1>(a, rp, nbuf, cpw, int(ntiles), s)
+                    : launch_dring3_c<1, 2>(a, rp, nbuf, cpw, int(ntiles), s);
+  return nch == 1 ? launch_dring3_c<2, 1>(a, rp, nbuf, cpw, int(ntiles), s)
+                  : launch_dring3_c<2, 2>(a, rp, nbuf, cpw, int(ntiles), s);
 }
 
 }  // namespace fce
