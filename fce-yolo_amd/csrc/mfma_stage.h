@@ -27,17 +27,27 @@ __device__ __forceinline__ void mfma_stage(const h8* wl, BL bl, EPI epi) {
   for (int i = 0; i < MF; ++i)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[i][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  // the fragments of step st + 1 are read while step st's MFMAs run (register double buffer; with the reads of a
+  // step issued only after the previous step's MFMAs, every step waited out a full LDS round trip at two waves per
+  // SIMD)
+  h8 av[2][CT], bv[2][MF];
+  auto load = [&](int st, h8 (&a)[CT], h8 (&b)[MF]) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) a[ct] = wl[(ct * NS + st) * 64];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) b[i] = bl(i, st);
+  };
+  load(0, av[0], bv[0]);
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
-    h8 av[CT], bv[MF];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) av[ct] = wl[(ct * NS + st) * 64];
-#pragma unroll
-    for (int i = 0; i < MF; ++i) bv[i] = bl(i, st);
+    if (st + 1 < NS) load(st + 1, av[(st + 1) & 1], bv[(st + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[ct], bv[i], acc[i][ct], 0, 0, 0);
+      for (int ct = 0; ct < CT; ++ct)
+        acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[st & 1][ct], bv[st & 1][i], acc[i][ct], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int i = 0; i < MF; ++i)
