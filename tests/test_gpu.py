@@ -1474,6 +1474,53 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
     assert err <= OP_TOL, err
 
 
+@pytest.mark.parametrize("cin,cout,stride,H,W,xpad,ypad,with_res", [
+    (64, 64, 1, 37, 41, 16, 8, True), (32, 32, 1, 45, 33, 32, 4, False), (64, 64, 2, 41, 37, 8, 24, True),
+    (32, 64, 2, 50, 30, 0, 2, True), (64, 96, 1, 19, 23, 64, 6, False)])
+def test_conv3x3_rings_on_channel_slice_views(cin, cout, stride, H, W, xpad, ypad, with_res, device):
+    """The persistent 3x3 rings (register ring 0x6xx, LDS-DMA ring 0xDxx) on the views the graph hands them: input,
+    output and residual as channel slices of wider NHWC buffers (ypad % 4 != 0: the LDS-DMA ring's unaligned-output
+    fallback to the register ring).  Bitwise equal to the default variant, the output buffer's other channels
+    untouched, fp64 parity."""
+    g = torch.Generator().manual_seed(cin * 31 + cout + stride + ypad)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (cin * 9) ** 0.5)
+    b = torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(2, cin, H, W, generator=g).half()
+    desc = N.ConvDesc(cin, cout, 3, stride, 1, N.ACT_SILU, 0, 0, None, 0, 0)
+    wp = M.pack_conv(desc, w, device)
+    bd = b.float().to(device)
+    xbuf = torch.randn(2, H, W, cin + xpad, generator=g).half().to(device)
+    xbuf[..., xpad:] = x.to(device).permute(0, 2, 3, 1)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    ref = torch.nn.functional.silu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, 1))
+    rt = None
+    if with_res:
+        r = torch.randn(2, cout, Ho, Wo, generator=g).half()
+        rbuf = torch.randn(2, Ho, Wo, cout + 8, generator=g).half().to(device)
+        rbuf[..., 8:] = r.to(device).permute(0, 2, 3, 1)
+        rt = N.Tensor(rbuf.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout + 8, 8)
+        ref = ref + r.double()
+    xt = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, 2, cin, H, W, cin + xpad, xpad)
+    codes = (C.c_int * 128)()
+    nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
+    rings = [c for c in codes[:nv] if (c & 0xF00) in (0x600, 0xD00)]
+    assert any((c & 0xF00) == 0xD00 for c in rings) and any((c & 0xF00) == 0x600 for c in rings)
+    outs = {}
+    for code in [-1] + rings:
+        y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
+        yt = N.Tensor(y.data_ptr(), N.F16, N.NHWC, 2, cout, Ho, Wo, cout + ypad, ypad)
+        N.call("fce_conv2d_variant", C.byref(desc), C.byref(xt), wp.data_ptr(), bd.data_ptr(),
+               C.byref(rt) if rt is not None else None, C.byref(yt), code, None)
+        yc = y.cpu()
+        assert torch.isnan(yc[..., :ypad]).all(), hex(code)
+        outs[code] = yc[..., ypad:].permute(0, 3, 1, 2)
+    base = outs[-1]
+    for code, y in outs.items():
+        assert torch.equal(y, base), (hex(code), (y.float() - base.float()).abs().max().item())
+    err = _rel(base, ref)
+    assert err <= OP_TOL, err
+
+
 @pytest.mark.parametrize("c,stride,H,W,cpad", [
     (64, 1, 80, 80, 0), (80, 1, 37, 45, 0), (80, 2, 41, 37, 0), (128, 1, 19, 23, 16), (256, 2, 20, 20, 0),
     (24, 1, 11, 9, 8), (64, 2, 7, 5, 0),
