@@ -140,6 +140,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
   };
 #pragma unroll
   for (int k = 0; k < NBUF - 1; ++k) issue(k, k);
+  // the A fragments and biases landed (with the prologue's copies) before the tile loop: otherwise hipcc's waitcnt
+  // pass, merging the loop's back edge with the entry, kept a counted vmcnt wait before nearly every MFMA of every tile
+  // (satisfied at once after the first tile: no time change measured, `profiles/r06_dring_probe.txt`)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   // vm ops per tile after its copies: CPW x RP residual loads, DPW copies, CPW x RP stores
   constexpr int NO = CPW * RP, PER = NO + DPW + NO;
   for (int k = 0; k < count; ++k) {
