@@ -126,7 +126,7 @@ class BneckDesc(C.Structure):
 
 
 class Pw2Desc(C.Structure):
-    """fce_pw2_desc: two chained 1x1 convs (w / b / act: op 1, op 2)."""
+    """fce_pw2_desc: two chained 1x1 convs (w / b / act: op 1, op 2; epi1 / fw / fn / fi: op 1's BiFPN epilogue)."""
     _fields_ = [
         ("cin1", C.c_int),
         ("cout1", C.c_int),
@@ -135,6 +135,10 @@ class Pw2Desc(C.Structure):
         ("act", C.c_int * 2),
         ("w", C.c_void_p * 2),
         ("b", C.c_void_p * 2),
+        ("epi1", C.c_int),
+        ("fw", C.c_void_p),
+        ("fn", C.c_int),
+        ("fi", C.c_int),
     ]
 
 

@@ -549,6 +549,7 @@ static void op_accesses(const fce_net* net, const OpDesc& op, std::vector<Access
     case OP_PW2:
       a.push_back({op.in, op.in_coff, op.in_coff + op.pw2.cin1, false});
       if (op.res >= 0) a.push_back({op.res, op.res_coff, op.res_coff + op.pw2.cout1, false});
+      if (op.pw2.epi1 == FCE_EPI_ACCUM) a.push_back({op.out, op.out_coff, op.out_coff + op.pw2.cout1, false});
       a.push_back({op.out, op.out_coff, op.out_coff + op.pw2.cout1, true});
       a.push_back({op.in2, op.in2_coff, op.in2_coff + op.pw2.cin2, false});
       if (op.res2 >= 0) a.push_back({op.res2, op.res2_coff, op.res2_coff + op.pw2.cout2, false});
@@ -714,6 +715,7 @@ void op_cost(const fce_net* net, const OpDesc& op, std::string* name, double* by
       const int lo = std::max(op.in2_coff, op.out_coff), hi = std::min(op.in2_coff + d.cin2, op.out_coff + d.cout1);
       const int over = op.in2 == op.out ? std::max(0, hi - lo) : 0;
       *bytes = px * 2 * (d.cin1 + (d.cin2 - over) + d.cout2 + (op.h_store ? d.cout1 : 0) + (op.res >= 0 ? d.cout1 : 0) +
+                         (d.epi1 == FCE_EPI_ACCUM ? d.cout1 : 0) +
                          (op.res2 >= 0 ? d.cout2 : 0) + (op.dup >= 0 ? op.dup_c : 0)) +
                double(conv_weight_bytes(c1)) + double(conv_weight_bytes(c2));
       *flops = 2.0 * px * (double(d.cin1) * d.cout1 + double(d.cin2) * d.cout2);
@@ -1027,7 +1029,10 @@ int fce_net_add_pw2_alt(fce_net* net, const fce_pw2_desc* d, int first_op) {
     const OpDesc& o = j ? o2 : o1;
     const fce_conv_desc& c = o.conv;
     FCE_CHECK(o.kind == OP_CONV && !o.skip && o.alt_first < 0 && o.in >= 0 && c.k == 1 && c.stride == 1 &&
-                  c.groups == 1 && c.up == 0 && c.epilogue == FCE_EPI_STORE && c.act == d->act[j] && c.cin == cins[j] &&
+                  c.groups == 1 && c.up == 0 && c.epilogue == (j ? FCE_EPI_STORE : d->epi1) && c.act == d->act[j] &&
+                  (j || d->epi1 == FCE_EPI_STORE ||
+                   (c.fusion_w == d->fw && c.fusion_n == d->fn && c.fusion_i == d->fi)) &&
+                  c.cin == cins[j] &&
                   c.cout == couts[j] && o.w == d->w[j] && o.b == d->b[j] && net->bufs[o.out].dtype == FCE_F16 &&
                   net->bufs[o.in].dtype == FCE_F16 && net->bufs[o.in].shift == net->bufs[o1.in].shift,
               "fce_net_add_pw2_alt: the two ops are not this pair's 1x1 convs (shapes, weights or epilogues differ)");

@@ -50,6 +50,9 @@ struct Pw2Args {
   const float* b1;
   const float* b2;
   int act1, act2;
+  int epi1;         // op 1: FCE_EPI_STORE, _WSTORE (scaled by the BiFPN weight) or _ACCUM (added to h's contents)
+  const float* fw;  // the BiFPN weights (epi1 != STORE)
+  int fn, fi;
 };
 
 // stage geometry: COUT couts over the tile's 4 pixel fragments with NW waves
@@ -177,6 +180,7 @@ __global__ __launch_bounds__(NW * 64, 1) void pw2_kernel(Pw2Args a) {
   }
   const float* bias1 = reinterpret_cast<const float*>(sm + OBIAS);
   const float* bias2 = bias1 + COUT1;
+  const float alpha1 = a.epi1 != FCE_EPI_STORE ? fusion_alpha(a.fw, a.fn, a.fi) : 1.f;  // conv_epilogue's weight
   _Float16* eimg = reinterpret_cast<_Float16*>(sm + OE);
 
   for (int t = t_begin; t < t_end; ++t) {
@@ -191,8 +195,9 @@ __global__ __launch_bounds__(NW * 64, 1) void pw2_kernel(Pw2Args a) {
         const int co0 = (cg * S1::CPW + cl) * 16 + grp * 4;
         const int u = (pg + S1::PG * i) * 16 + col, pix = p0 + u;
         const int pc = min(pix, a.P - 1);
-        h4 rv = h4{0, 0, 0, 0};
+        h4 rv = h4{0, 0, 0, 0}, pv = h4{0, 0, 0, 0};
         if (a.r1) rv = *reinterpret_cast<const h4*>(a.r1 + int64_t(pc) * a.r1cs + co0);
+        if (a.epi1 == FCE_EPI_ACCUM) pv = *reinterpret_cast<const h4*>(a.h + int64_t(pc) * a.hcs + co0);
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -202,6 +207,14 @@ __global__ __launch_bounds__(NW * 64, 1) void pw2_kernel(Pw2Args a) {
         if (a.r1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rv[j]);
+        }
+        // the BiFPN weighted store / accumulate, in conv_epilogue's arithmetic
+        if (a.epi1 == FCE_EPI_WSTORE) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] * alpha1);
+        } else if (a.epi1 == FCE_EPI_ACCUM) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fpin((float)pv[j] + fpin(alpha1 * v[j]));
         }
         const h4 hv = h4_of(v);
         if (co0 >= a.hs && co0 < a.hs + a.hn) {  // an op-2 input channel: into its image
@@ -245,8 +258,8 @@ __global__ __launch_bounds__(NW * 64, 1) void pw2_kernel(Pw2Args a) {
 }
 
 // ============================================================================ host
-// instantiated (cin1, cout1, cin2, cout2): the n scale's C3k2(c3k = True) pairs (L7: c 64; L10 / L24: c 128) and
-// its C2PSA's three pairs (c 128)
+// instantiated (cin1, cout1, cin2, cout2): the n scale's C3k2(c3k = True) pairs (L7: c 64; L10 / L24: c 128), its
+// C2PSA's three pairs (c 128) and two BiFPN realign -> C3k2 cv1 pairs of the neck
 struct PwInst {
   int cin1, cout1, cin2, cout2;
 };
@@ -259,6 +272,8 @@ static constexpr PwInst kPwInsts[] = {
     {256, 256, 128, 256},  // n L12 C2PSA cv1 -> attn.qkv
     {128, 128, 128, 256},  // n L12 attn.proj (+ b) -> ffn[0]
     {256, 128, 256, 256},  // n L12 ffn[1] (+ x1) -> cv2
+    {128, 64, 64, 128},    // n L14 -> L15: BiFPN_Concat's realign of L8 (ACCUM) -> C3k2 cv1
+    {128, 32, 32, 128},    // n L20 -> L21: the realign of L15 (ACCUM) -> C3k2 cv1
 };
 
 template <int CIN1, int COUT1, int CIN2, int COUT2>
@@ -328,6 +343,9 @@ int pw2_fused(const fce_pw2_desc& d, const fce_tensor& x1, const fce_tensor* r1,
             "pw2: op 2's input must take aligned channels of op 1's output");
   FCE_CHECK(!dup || (dup_lo % 8 == 0 && dup->c % 8 == 0 && dup_lo + dup->c <= d.cout2), "pw2: duplicate store range");
   FCE_CHECK(d.w[0] && d.w[1] && d.b[0] && d.b[1], "pw2: null weights");
+  FCE_CHECK(d.epi1 == FCE_EPI_STORE || ((d.epi1 == FCE_EPI_WSTORE || d.epi1 == FCE_EPI_ACCUM) && d.fw && d.fn > 0 &&
+                                         d.fi >= 0 && d.fi < d.fn),
+            "pw2: op 1's epilogue is a plain store or a BiFPN weighted store / accumulate with its weights");
   Pw2Args a{};
   a.x1 = static_cast<const _Float16*>(x1.data) + x1.coff;
   a.x1cs = x1.cstride;
@@ -358,7 +376,11 @@ int pw2_fused(const fce_pw2_desc& d, const fce_tensor& x1, const fce_tensor* r1,
   a.b2 = d.b[1];
   a.act1 = d.act[0] == FCE_ACT_SILU;
   a.act2 = d.act[1] == FCE_ACT_SILU;
-  static_assert(sizeof(kPwInsts) / sizeof(kPwInsts[0]) == 8, "pw2: one case per instance");
+  a.epi1 = d.epi1;
+  a.fw = d.fw;
+  a.fn = d.fn;
+  a.fi = d.fi;
+  static_assert(sizeof(kPwInsts) / sizeof(kPwInsts[0]) == 10, "pw2: one case per instance");
   switch (inst) {  // the template arguments are read from the table, so the two cannot disagree
     case 0: return pw_launch_i<0>(a, s);
     case 1: return pw_launch_i<1>(a, s);
@@ -367,7 +389,9 @@ int pw2_fused(const fce_pw2_desc& d, const fce_tensor& x1, const fce_tensor* r1,
     case 4: return pw_launch_i<4>(a, s);
     case 5: return pw_launch_i<5>(a, s);
     case 6: return pw_launch_i<6>(a, s);
-    default: return pw_launch_i<7>(a, s);
+    case 7: return pw_launch_i<7>(a, s);
+    case 8: return pw_launch_i<8>(a, s);
+    default: return pw_launch_i<9>(a, s);
   }
 }
 

@@ -318,11 +318,12 @@ def bneck_alt(be, blocks, x, y, first: int):
         be.bneck_alt(d, x, y, first, 2 * n)
 
 
-def pw2_alt(be, first: int, nat1, nat2):
+def pw2_alt(be, first: int, nat1, nat2, epi1=None):
     """Graph backend, after two 1x1 convs were emitted as ops first, first + 1 (the second reading channels of the
     first's output buffer; nat1 / nat2 their packed _ConvNative): where the channel counts are instantiated, record the
-    one-kernel pair (csrc/pw2.hip) as their alternative.  FCE_FUSE_PW2: unset / "auto" -- the plan keeps the faster,
-    "1" -- the fused kernel, "0" -- the two convs only."""
+    one-kernel pair (csrc/pw2.hip) as their alternative.  `epi1` = (epilogue, fusion weights ptr, n, i) when op 1 is a
+    BiFPN_Concat realign conv.  FCE_FUSE_PW2: unset / "auto" -- the plan keeps the faster, "1" -- the fused kernel,
+    "0" -- the two convs only."""
     import os
 
     if os.environ.get("FCE_FUSE_PW2", "auto") == "0" or be.shape_only or not hasattr(be, "pw2_alt"):
@@ -336,6 +337,8 @@ def pw2_alt(be, first: int, nat1, nat2):
             return
         d.act[j] = nat.desc.act
         d.w[j], d.b[j] = nat.w.data_ptr(), nat.b.data_ptr()
+    if epi1 is not None:
+        d.epi1, d.fw, d.fn, d.fi = epi1
     if N.lib().fce_pw2_supported(C.byref(d)):
         be.pw2_alt(d, first)
 
@@ -418,6 +421,9 @@ class C2f(nn.Module):
         """`bneck`: record each Bottleneck's one-kernel alternative (bneck_alt; off where the caller records the
         whole block's)."""
         c, n = self.c, len(self.m)
+        # a BiFPN_Concat whose last term is a realign conv, emitted just before and read here whole: that conv and cv1
+        # as a fused 1x1 pair (not where the block records its own one-kernel form, or cv1 opens a C3k pair)
+        bifpn = be.__dict__.pop("_bifpn_last", None)
         buf = be.alloc(x.n, (2 + n) * c, x.h, x.w)
         # the chunk the first block reads (and adds back) is a c-channel slice of the (2 + n) c record: when that
         # slice is narrower than a 128-byte line (c < 64), whole-graph lowering can also store it densely from
@@ -432,6 +438,8 @@ class C2f(nn.Module):
             self.cv1.emit(be, x, out=buf.slice(0, 2 * c))
         if n and isinstance(self.m[0], C3) and dense is None and k1 is not None and not be.shape_only:
             self.m[0]._pre_pair = (k1, _nat(self.cv1, be.device))  # cv1 -> the C3k's merged cv1 / cv2 (pw2_alt)
+        elif bifpn is not None and bneck and k1 is not None and bifpn[0] + 1 == k1 and bifpn[1] == (x.buf, x.coff, x.c, x.up):
+            pw2_alt(be, bifpn[0], bifpn[2], _nat(self.cv1, be.device), bifpn[3])  # realign (ACCUM) -> cv1
         for i, m in enumerate(self.m):
             src = dense if (i == 0 and dense is not None) else buf.slice((1 + i) * c, c)
             first = be.num_ops() if hasattr(be, "num_ops") else None
@@ -727,7 +735,11 @@ class BiFPN_Concat(nn.Module):
             if isinstance(m, nn.Identity):
                 be.wadd(x, y, (wp, n, i), accumulate=int(i > 0))
             else:
-                m.emit(be, x, out=y, epilogue=N.EPI_ACCUM if i else N.EPI_WSTORE, fusion=(wp, n, i))
+                k = be.num_ops() if hasattr(be, "num_ops") and not be.shape_only else None
+                epi = N.EPI_ACCUM if i else N.EPI_WSTORE
+                m.emit(be, x, out=y, epilogue=epi, fusion=(wp, n, i))
+                if k is not None and i == n - 1 and i > 0 and x.up == 0:  # the last term: a pair with the consumer's cv1
+                    be._bifpn_last = (k, (y.buf, y.coff, y.c, y.up), _nat(m, be.device), (epi, wp, n, i))
         return y
 
     def forward(self, x):

@@ -252,12 +252,18 @@ int fce_bneck_fused(const fce_bneck_desc* d, const fce_tensor* x, const fce_tens
  * pairs of C3k2 / C3k and C2PSA, block.py:303-307, :340, :1455-1464).  h is written to HBM when h_store (another op
  * reads it).  dup (nullable): op 2's output channels [dup_lo, dup_lo + dup.c) stored a second time (as
  * fce_conv2d_variant_dup).  act: FCE_ACT_SILU / FCE_ACT_NONE; w / b: the two convs' fce_conv_pack_weights images and
- * biases.  Bitwise equal to the two fce_conv2d calls.  fce_pw2_supported: the instantiated channel counts.  ABI v7. */
+ * biases.  epi1: op 1's epilogue, FCE_EPI_STORE (0), or FCE_EPI_WSTORE / FCE_EPI_ACCUM with the BiFPN weights fw
+ * (device, fn of them, this input's index fi) as fce_conv_desc takes them: op 1 is then a BiFPN_Concat realign conv
+ * (fce_block.py:57-63) whose weighted sum op 2 reads (ACCUM: h's previous contents are read and added).  Bitwise
+ * equal to the two fce_conv2d calls.  fce_pw2_supported: the instantiated channel counts.  ABI v7. */
 typedef struct fce_pw2_desc {
   int cin1, cout1, cin2, cout2;
   int act[2];
   const void* w[2];
   const float* b[2];
+  int epi1;
+  const float* fw;
+  int fn, fi;
 } fce_pw2_desc;
 int fce_pw2_supported(const fce_pw2_desc* d);
 int fce_pw2(const fce_pw2_desc* d, const fce_tensor* x1, const fce_tensor* r1, const fce_tensor* h, int h_store,

@@ -544,17 +544,17 @@ def test_fused_bneck_c_abi_views_and_parity(c, cm, nb, H, W, device):
 
 @pytest.mark.parametrize("batch,imgsz", [(2, 640), (3, 320), (1, (352, 288))])
 def test_fused_pw2_bitwise_equal_to_convs(batch, imgsz, device, monkeypatch):
-    """The one-kernel 1x1 pair (csrc/pw2.hip: the n scale's C3k2 cv1 -> C3k cv1 / cv2 and C3k cv3 -> cv2 pairs, and
-    C2PSA's cv1 -> qkv, proj (+ b) -> ffn[0], ffn[1] (+ x1) -> cv2) gives the forward bit for bit what the two convs
-    give: partial last pixel tiles (320, 352 x 288), op 1's output stored or not as the plan decides, and every form the
-    auto plan can pick."""
+    """The one-kernel 1x1 pair (csrc/pw2.hip: the n scale's C3k2 cv1 -> C3k cv1 / cv2 and C3k cv3 -> cv2 pairs,
+    C2PSA's cv1 -> qkv, proj (+ b) -> ffn[0], ffn[1] (+ x1) -> cv2, and the neck's BiFPN realign (accumulate) -> C3k2
+    cv1 pairs) gives the forward bit for bit what the two convs give: partial last pixel tiles (320, 352 x 288), op 1's
+    output stored or not as the plan decides, and every form the auto plan can pick."""
     model = cases.seeded_model("yolo11n-fce.yaml", 0).to(device)
     hw = (imgsz, imgsz) if isinstance(imgsz, int) else imgsz
     x = torch.rand(batch, 3, *hw, generator=torch.Generator().manual_seed(23)).half().to(device)
     monkeypatch.setenv("FCE_FUSE_PW2", "1")
     eng = Engine(model, batch, imgsz, device)
     alts = [i for i in range(eng.num_ops()) if eng.op_info(i)[0] == "pw2_fused"]
-    assert len(alts) == 9 and all(eng.alt_form(i) == 1 for i in alts)
+    assert len(alts) == 11 and all(eng.alt_form(i) == 1 for i in alts)
     yf = eng(x).clone()
     monkeypatch.setenv("FCE_FUSE_PW2", "0")
     eng2 = Engine(model, batch, imgsz, device)
@@ -573,21 +573,28 @@ def test_fused_pw2_bitwise_equal_to_convs(batch, imgsz, device, monkeypatch):
 
 
 @pytest.mark.parametrize("cin1,cout1,cin2,cout2,mode", [(128, 128, 64, 64, "pre"), (64, 64, 192, 128, "post"),
-                                                       (128, 128, 128, 256, "res"), (256, 128, 256, 256, "res_post")])
+                                                       (128, 128, 128, 256, "res"), (256, 128, 256, 256, "res_post"),
+                                                       (128, 64, 64, 128, "accum"), (128, 32, 32, 128, "wstore")])
 def test_fused_pw2_c_abi_views_and_parity(cin1, cout1, cin2, cout2, mode, device):
     """fce_pw2 through the C-ABI on channel-slice views of a 2 x 17 x 23 map (a partial 64-pixel tile): "pre" -- op 2
     reads the second half of op 1's output (with a duplicate store of its upper half), "post" -- op 2 reads [E | h] with
-    E from HBM, "res" / "res_post" -- op 1 without activation plus a residual (Attention.proj, ffn[1]); bit for bit the
-    two fce_conv2d calls, the channels outside the views untouched, h stored or not, and within the op tolerance of an
-    fp64 restatement."""
+    E from HBM, "res" / "res_post" -- op 1 without activation plus a residual (Attention.proj, ffn[1]), "accum" /
+    "wstore" -- op 1 a BiFPN realign conv (weighted accumulate into / weighted store of the sum op 2 reads whole); bit for
+    bit the two fce_conv2d calls, the channels outside the views untouched, h stored or not, and within the op
+    tolerance of an fp64 restatement."""
     n, H, W = 2, 17, 23
     g = torch.Generator().manual_seed(79)
     acts = (N.ACT_NONE if mode.startswith("res") else N.ACT_SILU, N.ACT_SILU)
+    fw = torch.tensor([0.7, -0.2, 1.3])
+    fwd = fw.to(device)
+    epi1 = {"accum": N.EPI_ACCUM, "wstore": N.EPI_WSTORE}.get(mode, N.EPI_STORE)
     ws, bs, descs, packed = [], [], [], []
-    for cin, cout, act in ((cin1, cout1, acts[0]), (cin2, cout2, acts[1])):
+    for j, (cin, cout, act) in enumerate(((cin1, cout1, acts[0]), (cin2, cout2, acts[1]))):
         w = torch.randn(cout, cin, 1, 1, generator=g) * (1.5 / cin ** 0.5)
         b = torch.randn(cout, generator=g) * 0.2
-        d = N.ConvDesc(cin, cout, 1, 1, 1, act, 0, N.EPI_STORE, None, 0, 0)
+        bifpn = j == 0 and epi1 != N.EPI_STORE
+        d = N.ConvDesc(cin, cout, 1, 1, 1, act, 0, epi1 if j == 0 else N.EPI_STORE, fwd.data_ptr() if bifpn else None,
+                       3 if bifpn else 0, 2 if bifpn else 0)
         ws.append(w), bs.append(b.float().to(device)), descs.append(d), packed.append(M.pack_conv(d, w, device))
     xbuf = torch.randn(n, H, W, cin1 + 32, generator=g).half().to(device)
     x1 = N.Tensor(xbuf.data_ptr(), N.F16, N.NHWC, n, cin1, H, W, cin1 + 32, 16)
@@ -618,6 +625,8 @@ def test_fused_pw2_c_abi_views_and_parity(cin1, cout1, cin2, cout2, mode, device
             d.cin1, d.cout1, d.cin2, d.cout2 = cin1, cout1, cin2, cout2
             for j in range(2):
                 d.act[j], d.w[j], d.b[j] = acts[j], packed[j].data_ptr(), bs[j].data_ptr()
+            if epi1 != N.EPI_STORE:
+                d.epi1, d.fw, d.fn, d.fi = epi1, fwd.data_ptr(), 3, 2
             assert N.lib().fce_pw2_supported(C.byref(d)) == 1
             N.call("fce_pw2", C.byref(d), C.byref(x1), C.byref(r1) if r1 else None, C.byref(ht), int(h_store),
                    C.byref(x2), None, C.byref(yt), C.byref(dt) if dt else None, dup_lo, stream)
@@ -646,6 +655,9 @@ def test_fused_pw2_c_abi_views_and_parity(cin1, cout1, cin2, cout2, mode, device
     if r1:
         t = t + rbuf[..., 8:8 + cout1].permute(0, 3, 1, 2).double().cpu()
     hb = base.cpu().permute(0, 3, 1, 2).double().clone()
+    if epi1 != N.EPI_STORE:
+        r = fw.clamp_min(0).double()
+        t = r[2] / (r.sum() + 1e-4) * t + (hb[:, hoff:hoff + cout1] if epi1 == N.EPI_ACCUM else 0)
     hb[:, hoff:hoff + cout1] = t.half().double()
     ref = F.silu(F.conv2d(hb[:, x2off:x2off + cin2], ws[1].double(), bs[1].double().cpu()))
     err = _rel(yf[..., 8:8 + cout2].permute(0, 3, 1, 2), ref)

@@ -306,10 +306,11 @@ def test_lowering_records_the_fused_alternatives(monkeypatch):
     names = [n for n, _ in ops]
     alts = [(i, n) for i, (n, f) in enumerate(ops) if f >= 0]
     assert all(ops[i][1] == 1 for i, _ in alts)
-    # stem; C3k2 L2, L4; L7 [pair, chain, pair]; L10 [pair, chain, pair]; C2PSA L12 three pairs; chain L15; C3k2 L18;
-    # chain L21; L24 [pair, chain, pair]; Detect cls P3, P4
+    # stem; C3k2 L2, L4; L7 [pair, chain, pair]; L10 [pair, chain, pair]; C2PSA L12 three pairs; L14 -> L15 [BiFPN
+    # realign -> cv1 pair, chain]; C3k2 L18; L20 -> L21 [pair, chain]; L24 [pair, chain, pair]; Detect cls P3, P4
     assert [n for _, n in alts] == (["stem_fused"] + ["c3k2_fused"] * 2 + ["pw2_fused", "bneck_fused", "pw2_fused"] * 2 +
-                                    ["pw2_fused"] * 3 + ["bneck_fused", "c3k2_fused", "bneck_fused"] +
+                                    ["pw2_fused"] * 3 + ["pw2_fused", "bneck_fused", "c3k2_fused", "pw2_fused",
+                                                         "bneck_fused"] +
                                     ["pw2_fused", "bneck_fused", "pw2_fused"] + ["detect_cls_fused"] * 2)
     assert names[:3] == ["conv_stem", "conv3x3_mfma", "stem_fused"]
     # the Bottleneck chains: C3k pairs (L7, L10, L24: four 3x3s) and the 40^2 neck blocks' single Bottleneck (L15, L21)
