@@ -10,7 +10,10 @@ namespace fce {
 // slot swizzle of the tile kernels (conv.hip tile_slot): an involution of the 4 * KP pieces of position u
 template <int KP>
 __device__ __forceinline__ int dr_slot(int u, int q) {
-  return KP == 1 ? (q ^ ((u >> 1) & 3)) : (q ^ (u & 6));
+  // KP 4 (16 pieces, 256 bytes per position: every position starts on bank 0): q ^ 2 (u & 7).  The lanes of a
+  // ds_read_b128 group read two pieces q0, q0 ^ 1 (their lane groups) at 8 consecutive positions each, so the XOR term
+  // takes all 8 even values per piece: 16 distinct 16-byte slots for any first position
+  return KP == 1 ? (q ^ ((u >> 1) & 3)) : KP == 2 ? (q ^ (u & 6)) : (q ^ ((u & 7) << 1));
 }
 
 static int dr_blocks_per_cu(const void* kernel, size_t lds) {
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
 
 template <int S, int RP, int NCH, int NBUF, int CPW>
 static int launch_dring3_k(const ConvArgs& a, int ntiles, hipStream_t s) {
-  if constexpr (!dring3_fits(S, RP, NCH, NBUF, CPW)) {
+  if constexpr (!dring3_offer(S, RP, NCH, NBUF, CPW)) {
     return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: configuration not instantiated");  // launch_dring3 checks first
   } else {
     constexpr size_t lds = size_t(NBUF) * Dring3Geom<S, RP, NCH, CPW == 1 ? 1 : 2>::BUF * 16;
@@ -241,14 +244,19 @@ static int launch_dring3_k(const ConvArgs& a, int ntiles, hipStream_t s) {
   }
 }
 
+template <int S, int RP, int NCH, int CPW>
+static int launch_dring3_b(const ConvArgs& a, int nbuf, int ntiles, hipStream_t s) {
+  return nbuf == 2 ? launch_dring3_k<S, RP, NCH, 2, CPW>(a, ntiles, s)
+                   : nbuf == 3 ? launch_dring3_k<S, RP, NCH, 3, CPW>(a, ntiles, s)
+                               : launch_dring3_k<S, RP, NCH, 4, CPW>(a, ntiles, s);
+}
+
 template <int S, int NCH, int CPW>
 static int launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int ntiles, hipStream_t s) {
-  if (rp == 2)
-    return nbuf == 3 ? launch_dring3_k<S, 2, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 2, NCH, 4, CPW>(a, ntiles, s);
-  if (rp == 4)
-    return nbuf == 3 ? launch_dring3_k<S, 4, NCH, 3, CPW>(a, ntiles, s) : launch_dring3_k<S, 4, NCH, 4, CPW>(a, ntiles, s);
-  if constexpr (CPW == 1)
-    return nbuf == 3 ? launch_dring3_k<S, 8, NCH, 3, 1>(a, ntiles, s) : launch_dring3_k<S, 8, NCH, 4, 1>(a, ntiles, s);
+  if (rp == 1) return launch_dring3_b<S, 1, NCH, CPW>(a, nbuf, ntiles, s);
+  if (rp == 2) return launch_dring3_b<S, 2, NCH, CPW>(a, nbuf, ntiles, s);
+  if (rp == 4) return launch_dring3_b<S, 4, NCH, CPW>(a, nbuf, ntiles, s);
+  if constexpr (CPW == 1) return launch_dring3_b<S, 8, NCH, 1>(a, nbuf, ntiles, s);
   return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: 8-row tiles need one cout tile per wave");
 }
 
@@ -259,9 +267,9 @@ static int launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int nti
 
 // nbuf: tile buffers of the LDS-DMA ring (nbuf - 1 tiles of input in flight ahead of the MFMAs); cpw: cout tiles per wave
 int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int stride, hipStream_t s) {
-  FCE_CHECK((a0.cin == 32 || a0.cin == 64) && a0.cout % (16 * cpw) == 0 && (rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) &&
-                (nbuf == 3 || nbuf == 4) && (cpw == 1 || cpw == 2) && (stride == 1 || stride == 2) &&
-                dring3_fits(stride, rp, a0.cin / 32, nbuf, cpw),
+  FCE_CHECK((a0.cin == 32 || a0.cin == 64 || a0.cin == 128) && a0.cout % (16 * cpw) == 0 &&
+                (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) && nbuf >= 2 && nbuf <= 4 &&
+                (cpw == 1 || cpw == 2) && (stride == 1 || stride == 2) && dring3_offer(stride, rp, a0.cin / 32, nbuf, cpw),
             "conv 3x3 LDS-DMA ring: bad configuration");
   FCE_CHECK(a0.vec_ok && int64_t(a0.P) * a0.ycs * 2 < (int64_t(1) << 31) &&
                 int64_t(a0.N) * a0.Hs * a0.Ws * a0.xcs * 2 < (int64_t(1) << 31),
@@ -274,9 +282,11 @@ int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int stride, hip
   const int nch = a.cin / 32;
   if (stride == 1)
     return nch == 1 ? launch_dring3_c<1, 1>(a, rp, nbuf, cpw, int(ntiles), s)
-                    : launch_dring3_c<1, 2>(a, rp, nbuf, cpw, int(ntiles), s);
+                    : nch == 2 ? launch_dring3_c<1, 2>(a, rp, nbuf, cpw, int(ntiles), s)
+                               : launch_dring3_c<1, 4>(a, rp, nbuf, cpw, int(ntiles), s);
   return nch == 1 ? launch_dring3_c<2, 1>(a, rp, nbuf, cpw, int(ntiles), s)
-                  : launch_dring3_c<2, 2>(a, rp, nbuf, cpw, int(ntiles), s);
+                  : nch == 2 ? launch_dring3_c<2, 2>(a, rp, nbuf, cpw, int(ntiles), s)
+                             : launch_dring3_c<2, 4>(a, rp, nbuf, cpw, int(ntiles), s);
 }
 
 }  // namespace fce

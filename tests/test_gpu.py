@@ -1488,11 +1488,12 @@ def test_conv_every_variant_bitwise_and_parity(case, device, monkeypatch):
 
 @pytest.mark.parametrize("cin,cout,stride,H,W,xpad,ypad,with_res", [
     (64, 64, 1, 37, 41, 16, 8, True), (32, 32, 1, 45, 33, 32, 4, False), (64, 64, 2, 41, 37, 8, 24, True),
-    (32, 64, 2, 50, 30, 0, 2, True), (64, 96, 1, 19, 23, 64, 6, False)])
+    (32, 64, 2, 50, 30, 0, 2, True), (64, 96, 1, 19, 23, 64, 6, False), (128, 128, 2, 41, 37, 16, 8, True),
+    (128, 64, 2, 21, 19, 0, 2, False)])
 def test_conv3x3_rings_on_channel_slice_views(cin, cout, stride, H, W, xpad, ypad, with_res, device):
     """The persistent 3x3 rings (register ring 0x6xx, LDS-DMA ring 0xDxx) on the views the graph hands them: input,
     output and residual as channel slices of wider NHWC buffers (ypad % 4 != 0: the LDS-DMA ring's unaligned-output
-    fallback to the register ring).  Bitwise equal to the default variant, the output buffer's other channels
+    fallback to the register ring, or at cin 128 to the implicit-GEMM kernel).  Bitwise equal to the default variant, the output buffer's other channels
     untouched, fp64 parity."""
     g = torch.Generator().manual_seed(cin * 31 + cout + stride + ypad)
     w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (cin * 9) ** 0.5)
@@ -1516,7 +1517,8 @@ def test_conv3x3_rings_on_channel_slice_views(cin, cout, stride, H, W, xpad, ypa
     codes = (C.c_int * 128)()
     nv = N.lib().fce_conv_variants(C.byref(desc), W, codes, 128)
     rings = [c for c in codes[:nv] if (c & 0xF00) in (0x600, 0xD00)]
-    assert any((c & 0xF00) == 0xD00 for c in rings) and any((c & 0xF00) == 0x600 for c in rings)
+    # cin 128: only the LDS-DMA ring's stride-2 one-row tiles (the register ring is cin 32 / 64)
+    assert any((c & 0xF00) == 0xD00 for c in rings) and any((c & 0xF00) == 0x600 for c in rings) == (cin < 128)
     outs = {}
     for code in [-1] + rings:
         y = torch.full((2, Ho, Wo, cout + ypad), float("nan"), dtype=torch.float16, device=device)
