@@ -2457,12 +2457,13 @@ int conv_tile_candidates(const fce_conv_desc& d, int det_box, int in_w, int* out
         if (n < cap) out[n++] = 0x600 | (rp << 4) | (pd - 1);
   if (d.k == 3 && (d.cin == 32 || d.cin == 64 || d.cin == 128) && d.cout % 16 == 0 && d.up == 0 && !det_box &&
       !no_ring() && !no_dring())
-    for (int cpw : {1, 2})  // persistent LDS-DMA ring: 0xD00 | rp << 4 | (cpw - 1) << 3 | (nbuf - 2)
+    for (int cpw : {1, 2})  // persistent LDS-DMA ring: 0xD00 | rp << 4 | (cpw - 1) << 3 | (sub - 1) << 2 | (nbuf - 2)
       for (int rp : {1, 2, 4, 8})
-        for (int nbuf : {2, 3, 4})
-          if (n < cap && d.cout % (16 * cpw) == 0 && (rp < 8 || cpw == 1) &&
-              dring3_offer(d.stride, rp, d.cin / 32, nbuf, cpw))
-            out[n++] = 0xD00 | (rp << 4) | ((cpw - 1) << 3) | (nbuf - 2);
+        for (int sub : {1, 2})
+          for (int nbuf : {2, 3, 4})
+            if (n < cap && d.cout % (16 * cpw) == 0 && (rp < 8 || cpw == 1) &&
+                dring3_offer(d.stride, rp, d.cin / 32, nbuf, cpw, sub))
+              out[n++] = 0xD00 | (rp << 4) | ((cpw - 1) << 3) | ((sub - 1) << 2) | (nbuf - 2);
   if (d.k == 3 && (d.cin == 32 || d.cin == 64) && d.cout % 32 == 0 && d.up == 0 && !det_box && !no_ring() &&
       !no_ring32())  // persistent 32x32x16 ring: 0x900 | rpw << 4 | log2(wc) << 12
     for (int wcl = 0; wcl < 3; ++wcl)
@@ -2974,10 +2975,10 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
   }
   if (kind == 13) {  // persistent 3x3 ring fed by LDS-DMA
     rp = (tile >> 4) & 15;
-    const int nbuf = (tile & 7) + 2, cpw = ((tile >> 3) & 1) + 1;
+    const int nbuf = (tile & 3) + 2, sub = ((tile >> 2) & 1) + 1, cpw = ((tile >> 3) & 1) + 1;
     FCE_CHECK(d.k == 3 && (d.cin == 32 || d.cin == 64 || d.cin == 128) && d.cout % (16 * cpw) == 0 &&
                   out_kind == OUT_F16 && d.up == 0 && (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) &&
-                  nbuf >= 2 && nbuf <= 4 && dring3_offer(d.stride, rp, d.cin / 32, nbuf, cpw),
+                  nbuf >= 2 && nbuf <= 4 && dring3_offer(d.stride, rp, d.cin / 32, nbuf, cpw, sub),
               "conv: bad 3x3 LDS-DMA ring hint");
     // the copies and the unconditional stores address input and output through buffer resources (byte offsets < 2^31),
     // the output as 8-byte pieces: other views take the register ring, which gives the same bits
@@ -2985,7 +2986,7 @@ int conv2d_impl(const fce_conv_desc& d, const fce_tensor& x, const void* w, cons
         int64_t(a.N) * a.Hs * a.Ws * a.xcs * 2 >= (int64_t(1) << 31))  // cin 128: the implicit-GEMM kernel (same bits)
       return d.cin == 128 ? conv2d_impl(d, x, w, bias, res, y, det, s, -1, dup, duplo)
                           : launch_ring3(a, std::max(rp, 2) > 4 ? 4 : std::max(rp, 2), 1, d.stride, s);
-    return launch_dring3(a, rp, nbuf, cpw, d.stride, s);
+    return launch_dring3(a, rp, nbuf, cpw, sub, d.stride, s);
   }
   if (kind == 9) {  // persistent 3x3 ring on 32x32x16 MFMAs
     const int rpw = (tile >> 4) & 15, wc = 1 << ((tile >> 12) & 3);

@@ -1,7 +1,11 @@
-// Persistent 3x3 convolution ring fed by LDS-DMA (variant code 0xD00 | rp << 4 | (nbuf - 2) of fce_conv2d_variant).
+// Persistent 3x3 convolution ring fed by LDS-DMA (variant code 0xD00 | rp << 4 | (cpw - 1) << 3 | (sub - 1) << 2 |
+// (nbuf - 2) of fce_conv2d_variant).
 // Replaces (reference, ultralytics/): nn/modules/conv.py:39-89 Conv.forward_fuse (3x3, BN folded by
 // utils/torch_utils.py:237-267) for cin 32 / 64, like conv3x3_ring_kernel (csrc/conv.hip), bitwise identical to it.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "conv_args.h"
 
@@ -14,6 +18,14 @@ __device__ __forceinline__ int dr_slot(int u, int q) {
   // ds_read_b128 group read two pieces q0, q0 ^ 1 (their lane groups) at 8 consecutive positions each, so the XOR term
   // takes all 8 even values per piece: 16 distinct 16-byte slots for any first position
   return KP == 1 ? (q ^ ((u >> 1) & 3)) : KP == 2 ? (q ^ (u & 6)) : (q ^ ((u & 7) << 1));
+}
+
+static bool dr_timing() {
+  static const bool v = [] {
+    const char* e = getenv("FCE_DRING_TIMING");
+    return e && atoi(e) != 0;
+  }();
+  return v;
 }
 
 static int dr_blocks_per_cu(const void* kernel, size_t lds) {
@@ -72,10 +84,12 @@ __device__ __forceinline__ void dr_vm_wait(int n) {
 // 2 -- two waves along the couts x two along the rows, each B fragment feeding two MFMAs (half the LDS reads per
 // MFMA: the bound of the 64 -> 64 stride-1 convs), the A fragments of both cout tiles in registers (no staging
 // registers to make room for: the copies go straight to LDS).
-template <int S, int RP, int NCH, int NBUF, int CPW>
-__global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int nslot) {
-  constexpr int WC = CPW == 1 ? 4 : 2, WRW = 4 / WC;
-  using G = Dring3Geom<S, RP, NCH, WRW>;
+// TM (diagnostics, FCE_DRING_TIMING=1): per wave, the clocks of each tile's phases summed over its tiles -- the wait for
+// its copies plus the barrier, the residual loads and copy issue, the MFMA loop, the epilogue -- for the first 4096 blocks
+template <int S, int RP, int NCH, int NBUF, int CPW, int SUB = 1, bool TM = false>
+__global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int nslot, unsigned long long* tm) {
+  constexpr int WC = CPW == 1 ? 4 : 2, WRW = 4 / WC, RPT = RP * SUB;  // RPT rows per wave and tile
+  using G = Dring3Geom<S, RPT, NCH, WRW>;
   constexpr int TW = G::TW, TH = G::TH, CI = G::CI, NQ = G::NQ, NE = G::NE, DPW = G::DPW, BUF = G::BUF;
   constexpr int KP = NCH;
   extern __shared__ __attribute__((aligned(16))) h8 dring_smem[];  // NBUF x BUF pieces
@@ -147,8 +161,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
   // pass, merging the loop's back edge with the entry, kept a counted vmcnt wait before nearly every MFMA of every tile
   // (satisfied at once after the first tile: no time change measured, `profiles/r06_dring_probe.txt`)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  // vm ops per tile after its copies: CPW x RP residual loads, DPW copies, CPW x RP stores
-  constexpr int NO = CPW * RP, PER = NO + DPW + NO;
+  // vm ops per tile after its copies: CPW x RPT residual loads, DPW copies, CPW x RPT stores
+  constexpr int NO = CPW * RPT, PER = NO + DPW + NO;
+  unsigned long long ph[4] = {0, 0, 0, 0}, tprev = 0;
+  auto tick = [&](int i) {
+    if constexpr (TM) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[i] += t - tprev;
+      tprev = t;
+    }
+  };
+  if constexpr (TM) tprev = __builtin_amdgcn_s_memtime();
   for (int k = 0; k < count; ++k) {
     // this wave's copies of tile k are older than: the prologue's later copies and k earlier tiles (k < NBUF - 1), or
     // the stores of the tile that issued them and NBUF - 2 whole tiles since
@@ -156,137 +179,193 @@ __global__ __launch_bounds__(256, 2) void conv3x3_dring_kernel(ConvArgs a, int n
     dr_vm_wait(newer);
     __builtin_amdgcn_s_barrier();  // every wave's copies of tile k landed; tile k - 1's reads are done
     asm volatile("" ::: "memory");
+    tick(3);
     const int tt = tbeg + k * step;
     const int tx = tt % tiles_x, r0 = tt / tiles_x, ty = r0 % tiles_y, n = r0 / tiles_y;
-    const int oy0 = ty * TH + wr * RP, ox = tx * TW + col;
-    const int pix0 = (n * a.Ho + oy0) * a.Wo + ox;  // output pixel of row p: pix0 + p Wo (< 2^30: the output < 2 GiB)
+    const int oy0 = ty * TH + wr * RPT, ox = tx * TW + col;  // the wave's first output row (SUB sub-tiles of RP rows)
+    const int pix0 = (n * a.Ho + oy0) * a.Wo + ox;  // output pixel of row q: pix0 + q Wo (< 2^30: the output < 2 GiB)
     // residuals first (clamped, unconditional: the zero line without one), then the copies of tile k + NBUF - 1 into
     // the buffer tile k - 1 used: the epilogue's wait for the residuals leaves those copies in flight
-    h4 rres[CPW][RP];
+    h4 rres[CPW][RPT];
 #pragma unroll
     for (int cl = 0; cl < CPW; ++cl)
 #pragma unroll
-      for (int p = 0; p < RP; ++p) {
-        const int pix = (n * a.Ho + min(oy0 + p, a.Ho - 1)) * a.Wo + min(ox, a.Wo - 1);
-        rres[cl][p] = *reinterpret_cast<const h4*>(rbase + int64_t(pix) * rcs + (a.res ? co0[cl] : 0));
+      for (int q = 0; q < RPT; ++q) {
+        const int pix = (n * a.Ho + min(oy0 + q, a.Ho - 1)) * a.Wo + min(ox, a.Wo - 1);
+        rres[cl][q] = *reinterpret_cast<const h4*>(rbase + int64_t(pix) * rcs + (a.res ? co0[cl] : 0));
       }
     issue(k + NBUF - 1, (k + NBUF - 1) % NBUF);
+    tick(0);
     const h8* const img = dring_smem + (k % NBUF) * BUF;
-    f4 acc[CPW][RP];
 #pragma unroll
-    for (int cl = 0; cl < CPW; ++cl)
+    for (int sb = 0; sb < SUB; ++sb) {  // sub-tiles: more MFMAs per barrier and copy wait, the same registers
+      f4 acc[CPW][RP];
 #pragma unroll
-      for (int p = 0; p < RP; ++p) acc[cl][p] = f4{0.f, 0.f, 0.f, 0.f};
-    // K-steps (chunk, tap) in the ring's order; the B fragments of step s + 1 are read while step s's MFMAs run (a
-    // register double buffer: without it hipcc waited lgkmcnt(0) before nearly every MFMA group, and at two waves per
-    // SIMD the LDS latency, not the LDS bandwidth, set the rate)
-    auto read_b = [&](int st, h8 (&bv)[RP]) {
-      const int kc = st / 9, tap = st - kc * 9, ky = tap / 3, kx = tap - ky * 3;
+      for (int cl = 0; cl < CPW; ++cl)
 #pragma unroll
-      for (int p = 0; p < RP; ++p) {
-        const int u = ((wr * RP + p) * S + ky) * CI + tile_col<S, CI>(col * S + kx);
-        bv[p] = img[u * NQ + dr_slot<KP>(u, kc * 4 + grp)];
+        for (int p = 0; p < RP; ++p) acc[cl][p] = f4{0.f, 0.f, 0.f, 0.f};
+      // K-steps (chunk, tap) in the ring's order; the B fragments of step s + 1 are read while step s's MFMAs run (a
+      // register double buffer: without it hipcc waited lgkmcnt(0) before nearly every MFMA group)
+      // a sub-tile RP S CI positions on (a multiple of 8: the same swizzle) reads at a constant offset from the first's
+      // addresses, which the ds reads take as an immediate (recomputed addresses per sub-tile spilled)
+      constexpr bool SHIFT = (RP * S * CI) % 8 == 0;
+      auto read_b = [&](int st, h8 (&bv)[RP]) {
+        const int kc = st / 9, tap = st - kc * 9, ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const int u = ((wr * RPT + (SHIFT ? 0 : sb * RP) + p) * S + ky) * CI + tile_col<S, CI>(col * S + kx);
+          bv[p] = img[(SHIFT ? sb * RP * S * CI * NQ : 0) + u * NQ + dr_slot<KP>(u, kc * 4 + grp)];
+        }
+      };
+      h8 bb[2][RP];
+      read_b(0, bb[0]);
+#pragma unroll
+      for (int st = 0; st < NCH * 9; ++st) {
+        if (st + 1 < NCH * 9) read_b(st + 1, bb[(st + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // the next step's reads ahead of this step's MFMAs
+#pragma unroll
+        for (int p = 0; p < RP; ++p)
+#pragma unroll
+          for (int cl = 0; cl < CPW; ++cl)
+            acc[cl][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cl][st], bb[st & 1][p], acc[cl][p], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    };
-    h8 bb[2][RP];
-    read_b(0, bb[0]);
+      // epilogue: tile3_post's arithmetic (bias, SiLU, residual, fp16), every lane storing (dropped past the edges)
+      if (sb == 0) {
+        tick(1);
+        dr_vm_wait(DPW);  // the residuals (older than this tile's copies)
+      }
 #pragma unroll
-    for (int st = 0; st < NCH * 9; ++st) {
-      if (st + 1 < NCH * 9) read_b(st + 1, bb[(st + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);  // the next step's reads ahead of this step's MFMAs
+      for (int cl = 0; cl < CPW; ++cl)
 #pragma unroll
-      for (int p = 0; p < RP; ++p)
+        for (int p = 0; p < RP; ++p) {
+          const int q = sb * RP + p, oy = oy0 + q;
+          float v[4];
 #pragma unroll
-        for (int cl = 0; cl < CPW; ++cl)
-          acc[cl][p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cl][st], bb[st & 1][p], acc[cl][p], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+          for (int j = 0; j < 4; ++j) {
+            const float t = acc[cl][p][j] + bz[cl][j];
+            v[j] = a.act ? silu(t) : t;
+          }
+          if (a.res) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rres[cl][q][j]);
+          }
+          const bool ok = cok[cl] && oy < a.Ho && ox < a.Wo;
+          const uint32_t off = uint32_t((pix0 + q * a.Wo) * a.ycs + co0[cl]) * 2u;
+          store_h4_or_drop(yr, ok, off,
+                           h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])});
+        }
+      // one sub-tile's accumulators live at a time (interleaving the next one's MFMAs with this epilogue spilled)
+      if (SUB > 1) __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue: tile3_post's arithmetic (bias, SiLU, residual, fp16), every lane storing (dropped past the edges)
-    dr_vm_wait(DPW);  // the residuals (older than this tile's copies)
-#pragma unroll
-    for (int cl = 0; cl < CPW; ++cl)
-#pragma unroll
-      for (int p = 0; p < RP; ++p) {
-        const int oy = oy0 + p;
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float t = acc[cl][p][j] + bz[cl][j];
-          v[j] = a.act ? silu(t) : t;
-        }
-        if (a.res) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fpin(v[j] + (float)rres[cl][p][j]);
-        }
-        const bool ok = cok[cl] && oy < a.Ho && ox < a.Wo;
-        const uint32_t off = uint32_t((pix0 + p * a.Wo) * a.ycs + co0[cl]) * 2u;
-        store_h4_or_drop(yr, ok, off, h4{(_Float16)fpin(v[0]), (_Float16)fpin(v[1]), (_Float16)fpin(v[2]), (_Float16)fpin(v[3])});
-      }
+    tick(2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no copy may land in LDS after the block is gone
+  if constexpr (TM) {
+    tick(3);
+    if (lane == 0 && blockIdx.x < 4096) {
+      unsigned long long* o = tm + (size_t(blockIdx.x) * 4 + wave) * 5;
+      for (int i = 0; i < 4; ++i) o[i] = ph[i];
+      o[4] = count;
+    }
+  }
 }
 
-template <int S, int RP, int NCH, int NBUF, int CPW>
+template <int S, int RP, int NCH, int NBUF, int CPW, int SUB>
 static int launch_dring3_k(const ConvArgs& a, int ntiles, hipStream_t s) {
-  if constexpr (!dring3_offer(S, RP, NCH, NBUF, CPW)) {
+  if constexpr (!dring3_offer(S, RP, NCH, NBUF, CPW, SUB)) {
     return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: configuration not instantiated");  // launch_dring3 checks first
   } else {
-    constexpr size_t lds = size_t(NBUF) * Dring3Geom<S, RP, NCH, CPW == 1 ? 1 : 2>::BUF * 16;
-    auto k = conv3x3_dring_kernel<S, RP, NCH, NBUF, CPW>;
+    constexpr size_t lds = size_t(NBUF) * Dring3Geom<S, RP * SUB, NCH, CPW == 1 ? 1 : 2>::BUF * 16;
+    auto k = conv3x3_dring_kernel<S, RP, NCH, NBUF, CPW, SUB>;
     static const bool big = lds <= 64 * 1024 || hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                      160 * 1024) == hipSuccess;
     if (!big) return fail(FCE_ERR_HIP, "conv 3x3 LDS-DMA ring: cannot opt in to >64 KiB LDS");
     static const int occ = dr_blocks_per_cu(reinterpret_cast<const void*>(k), lds);
     const int nslot = dr_slots(ntiles, a.gy, occ);
-    FCE_LAUNCH(k, dim3(unsigned(8 * a.gy * nslot)), dim3(256), lds, s, a, nslot);
+    const unsigned grid = unsigned(8 * a.gy * nslot);
+    if (!dr_timing()) {
+      FCE_LAUNCH(k, dim3(grid), dim3(256), lds, s, a, nslot, nullptr);
+      return launch_status("conv3x3_dring_kernel");
+    }
+    // diagnostics: one timed launch, synchronised, the per-tile phase clocks (averaged over waves) on stderr
+    auto kt = conv3x3_dring_kernel<S, RP, NCH, NBUF, CPW, SUB, true>;
+    if (lds > 64 * 1024)
+      FCE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kt), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+    static unsigned long long* tm = nullptr;
+    const size_t nrec = size_t(4096) * 4 * 5;
+    if (!tm) FCE_HIP_CHECK(hipMalloc(&tm, nrec * 8));
+    FCE_HIP_CHECK(hipMemsetAsync(tm, 0, nrec * 8, s));
+    hipLaunchKernelGGL(kt, dim3(grid), dim3(256), lds, s, a, nslot, tm);
+    FCE_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(nrec);
+    FCE_HIP_CHECK(hipMemcpy(h.data(), tm, nrec * 8, hipMemcpyDeviceToHost));
+    double ph[4] = {0, 0, 0, 0}, tiles = 0;
+    for (size_t i = 0; i < nrec / 5; ++i) {
+      for (int j = 0; j < 4; ++j) ph[j] += double(h[i * 5 + j]);
+      tiles += double(h[i * 5 + 4]);
+    }
+    if (tiles > 0)
+      fprintf(stderr, "dring<S%d,RP%d,NCH%d,NBUF%d,CPW%d,SUB%d> grid %u, %.2f tiles per wave; clocks per tile: res+copy issue %.0f, "
+              "mfma %.0f, epilogue %.0f, wait+barrier %.0f\n", S, RP, NCH, NBUF, CPW, SUB, grid, tiles / (nrec / 5 > grid * 4 ? grid * 4 : nrec / 5),
+              ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles);
     return launch_status("conv3x3_dring_kernel");
   }
 }
 
+template <int S, int RP, int NCH, int CPW, int SUB>
+static int launch_dring3_u(const ConvArgs& a, int nbuf, int ntiles, hipStream_t s) {
+  return nbuf == 2 ? launch_dring3_k<S, RP, NCH, 2, CPW, SUB>(a, ntiles, s)
+                   : nbuf == 3 ? launch_dring3_k<S, RP, NCH, 3, CPW, SUB>(a, ntiles, s)
+                               : launch_dring3_k<S, RP, NCH, 4, CPW, SUB>(a, ntiles, s);
+}
+
 template <int S, int RP, int NCH, int CPW>
-static int launch_dring3_b(const ConvArgs& a, int nbuf, int ntiles, hipStream_t s) {
-  return nbuf == 2 ? launch_dring3_k<S, RP, NCH, 2, CPW>(a, ntiles, s)
-                   : nbuf == 3 ? launch_dring3_k<S, RP, NCH, 3, CPW>(a, ntiles, s)
-                               : launch_dring3_k<S, RP, NCH, 4, CPW>(a, ntiles, s);
+static int launch_dring3_b(const ConvArgs& a, int nbuf, int sub, int ntiles, hipStream_t s) {
+  return sub == 1 ? launch_dring3_u<S, RP, NCH, CPW, 1>(a, nbuf, ntiles, s)
+                  : launch_dring3_u<S, RP, NCH, CPW, 2>(a, nbuf, ntiles, s);
 }
 
 template <int S, int NCH, int CPW>
-static int launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int ntiles, hipStream_t s) {
-  if (rp == 1) return launch_dring3_b<S, 1, NCH, CPW>(a, nbuf, ntiles, s);
-  if (rp == 2) return launch_dring3_b<S, 2, NCH, CPW>(a, nbuf, ntiles, s);
-  if (rp == 4) return launch_dring3_b<S, 4, NCH, CPW>(a, nbuf, ntiles, s);
-  if constexpr (CPW == 1) return launch_dring3_b<S, 8, NCH, 1>(a, nbuf, ntiles, s);
+static int launch_dring3_s(const ConvArgs& a, int rp, int nbuf, int sub, int ntiles, hipStream_t s) {
+  if (rp == 1) return launch_dring3_b<S, 1, NCH, CPW>(a, nbuf, sub, ntiles, s);
+  if (rp == 2) return launch_dring3_b<S, 2, NCH, CPW>(a, nbuf, sub, ntiles, s);
+  if (rp == 4) return launch_dring3_b<S, 4, NCH, CPW>(a, nbuf, sub, ntiles, s);
+  if constexpr (CPW == 1) return launch_dring3_b<S, 8, NCH, 1>(a, nbuf, sub, ntiles, s);
   return fail(FCE_ERR_INVALID, "conv 3x3 LDS-DMA ring: 8-row tiles need one cout tile per wave");
 }
 
 template <int S, int NCH>
-static int launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int ntiles, hipStream_t s) {
-  return cpw == 1 ? launch_dring3_s<S, NCH, 1>(a, rp, nbuf, ntiles, s) : launch_dring3_s<S, NCH, 2>(a, rp, nbuf, ntiles, s);
+static int launch_dring3_c(const ConvArgs& a, int rp, int nbuf, int cpw, int sub, int ntiles, hipStream_t s) {
+  return cpw == 1 ? launch_dring3_s<S, NCH, 1>(a, rp, nbuf, sub, ntiles, s)
+                  : launch_dring3_s<S, NCH, 2>(a, rp, nbuf, sub, ntiles, s);
 }
 
 // nbuf: tile buffers of the LDS-DMA ring (nbuf - 1 tiles of input in flight ahead of the MFMAs); cpw: cout tiles per wave
-int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int stride, hipStream_t s) {
+int launch_dring3(const ConvArgs& a0, int rp, int nbuf, int cpw, int sub, int stride, hipStream_t s) {
   FCE_CHECK((a0.cin == 32 || a0.cin == 64 || a0.cin == 128) && a0.cout % (16 * cpw) == 0 &&
                 (rp == 1 || rp == 2 || rp == 4 || (rp == 8 && cpw == 1)) && nbuf >= 2 && nbuf <= 4 &&
-                (cpw == 1 || cpw == 2) && (stride == 1 || stride == 2) && dring3_offer(stride, rp, a0.cin / 32, nbuf, cpw),
+                (cpw == 1 || cpw == 2) && (sub == 1 || sub == 2) && (stride == 1 || stride == 2) &&
+                dring3_offer(stride, rp, a0.cin / 32, nbuf, cpw, sub),
             "conv 3x3 LDS-DMA ring: bad configuration");
   FCE_CHECK(a0.vec_ok && int64_t(a0.P) * a0.ycs * 2 < (int64_t(1) << 31) &&
                 int64_t(a0.N) * a0.Hs * a0.Ws * a0.xcs * 2 < (int64_t(1) << 31),
             "conv 3x3 LDS-DMA ring: 8-byte aligned output, input and output below 2 GiB (the caller takes the register ring otherwise)");
   ConvArgs a = a0;
-  const int th = rp * cpw;  // cpw 2: two waves along the rows
+  const int th = rp * cpw * sub;  // cpw 2: two waves along the rows
   const int64_t ntiles = int64_t((a.Wo + 15) / 16) * ((a.Ho + th - 1) / th) * a.N;
   FCE_CHECK(ntiles < (int64_t(1) << 30), "conv 3x3 LDS-DMA ring: too many tiles");
   a.gy = ((a.cout + 15) / 16 + 3) / 4;  // 4 cout tiles per block either way
   const int nch = a.cin / 32;
   if (stride == 1)
-    return nch == 1 ? launch_dring3_c<1, 1>(a, rp, nbuf, cpw, int(ntiles), s)
-                    : nch == 2 ? launch_dring3_c<1, 2>(a, rp, nbuf, cpw, int(ntiles), s)
-                               : launch_dring3_c<1, 4>(a, rp, nbuf, cpw, int(ntiles), s);
-  return nch == 1 ? launch_dring3_c<2, 1>(a, rp, nbuf, cpw, int(ntiles), s)
-                  : nch == 2 ? launch_dring3_c<2, 2>(a, rp, nbuf, cpw, int(ntiles), s)
-                             : launch_dring3_c<2, 4>(a, rp, nbuf, cpw, int(ntiles), s);
+    return nch == 1 ? launch_dring3_c<1, 1>(a, rp, nbuf, cpw, sub, int(ntiles), s)
+                    : nch == 2 ? launch_dring3_c<1, 2>(a, rp, nbuf, cpw, sub, int(ntiles), s)
+                               : launch_dring3_c<1, 4>(a, rp, nbuf, cpw, sub, int(ntiles), s);
+  return nch == 1 ? launch_dring3_c<2, 1>(a, rp, nbuf, cpw, sub, int(ntiles), s)
+                  : nch == 2 ? launch_dring3_c<2, 2>(a, rp, nbuf, cpw, sub, int(ntiles), s)
+                             : launch_dring3_c<2, 4>(a, rp, nbuf, cpw, sub, int(ntiles), s);
 }
 
 }  // namespace fce

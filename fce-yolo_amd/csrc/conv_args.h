@@ -432,9 +432,10 @@ static constexpr bool big3_ok(int s, int wm, int ab, int nw = 4) {
   return nw == 4 && (ab == 2 || ab == 3) && (s == 1 ? (wm == 1 || wm == 2) : wm == 2);
 }
 int launch_big3(const ConvArgs& a, int wm, int ab, int nw, int stride, int n, hipStream_t s);
-// Persistent 3x3 ring fed by LDS-DMA (conv3x3_dring.hip), coded 0xD00 | rp << 4 | (cpw - 1) << 3 | (nbuf - 2): cin
-// 32 / 64 / 128, cpw cout tiles per wave (1: 4 waves along the couts; 2: 2 x 2 waves), rp rows x 16 columns per wave,
-// nbuf LDS tile buffers (nbuf - 1 tiles of input in flight)
+// Persistent 3x3 ring fed by LDS-DMA (conv3x3_dring.hip), coded 0xD00 | rp << 4 | (cpw - 1) << 3 | (sub - 1) << 2 |
+// (nbuf - 2): cin 32 / 64 / 128, cpw cout tiles per wave (1: 4 waves along the couts; 2: 2 x 2 waves), sub x rp rows x
+// 16 columns per wave and tile (sub sub-tiles of rp rows, one after the other, per barrier), nbuf LDS tile buffers
+// (nbuf - 1 tiles of input in flight)
 template <int S, int RP, int NCH, int WRW = 1>
 struct Dring3Geom {
   static constexpr int TW = 16, TH = WRW * RP;  // WRW waves along the rows (2 when each wave owns 2 cout tiles)
@@ -445,20 +446,23 @@ struct Dring3Geom {
   static constexpr int BUF = DPW * 4 * 64;     // pieces per tile buffer
 };
 
-static constexpr bool dring3_fits(int s, int rp, int nch, int nbuf, int cpw = 1) {
-  return size_t(nbuf) * ((((((cpw * rp - 1) * s + 3) * (15 * s + 3) * 4 * nch + 63) / 64 + 3) / 4) * 4 * 64) * 16 <=
+static constexpr bool dring3_fits(int s, int rp, int nch, int nbuf, int cpw = 1, int sub = 1) {
+  return size_t(nbuf) * ((((((cpw * rp * sub - 1) * s + 3) * (15 * s + 3) * 4 * nch + 63) / 64 + 3) / 4) * 4 * 64) * 16 <=
              80 * 1024 &&       // two blocks per CU
          (cpw == 1 || nch == 1) &&               // two cout tiles of 64-channel A fragments spill at two waves
          (rp < 8 || (nch == 1 && nbuf == 3)) &&  // per SIMD, and so do 8-row tiles of them (or with four buffers)
-         (nch < 4 || (s == 2 && rp == 1));  // 128 channels (36 A fragments in registers): stride-2 one-row tiles
-}                                        // only; the two-row stride-1 ones spilled (31.2 against 24.3 us, r06al)
+         (nch < 4 || (s == 2 && rp == 1)) &&  // 128 channels (36 A fragments in registers): stride-2 one-row tiles
+         (sub == 1 || (sub == 2 && rp * sub <= 8));  // only; the two-row stride-1 ones spilled (31.2 against 24.3 us,
+}                                                    // r06al); sub-tiles: 8 rows of held residuals at most
 // the candidates offered: two buffers or one-row tiles only for the 128-channel tiles, which need them to fit (at 32 /
-// 64 channels the two-buffer ones are the big stride-2 tiles, which spill)
-static constexpr bool dring3_offer(int s, int rp, int nch, int nbuf, int cpw = 1) {
-  return dring3_fits(s, rp, nch, nbuf, cpw) && (nch == 4 || (nbuf > 2 && rp > 1)) &&
-         (nbuf > 2 || !dring3_fits(s, rp, nch, 3, cpw));
+// 64 channels the two-buffer ones are the big stride-2 tiles, which spill); two sub-tiles only for the 32-channel
+// stride-1 convs, the one place they measured ahead (48.4 against 49.9 us at 160 x 160; 64 -> 64 at 80 x 80 and the
+// stride-2 ones slower, the 64-channel 8-row tiles spilling: profiles/r06_dring_probe.txt)
+static constexpr bool dring3_offer(int s, int rp, int nch, int nbuf, int cpw = 1, int sub = 1) {
+  return dring3_fits(s, rp, nch, nbuf, cpw, sub) && (nch == 4 || (nbuf > 2 && rp > 1)) &&
+         (nbuf > 2 || !dring3_fits(s, rp, nch, 3, cpw, sub)) && (sub == 1 || (nbuf > 2 && rp >= 2 && nch == 1 && s == 1));
 }
-int launch_dring3(const ConvArgs& a, int rp, int nbuf, int cpw, int stride, hipStream_t s);
+int launch_dring3(const ConvArgs& a, int rp, int nbuf, int cpw, int sub, int stride, hipStream_t s);
 // Wide-tile 3x3 (conv3x3_wide.hip), coded 0xA00 | log2(cw) << 4: 64 cw couts x 16 (4 / cw) rows per block
 bool wide3_ok(int stride, int cw);
 int launch_wide3(const ConvArgs& a, int cw, int stride, int n, hipStream_t s);
