@@ -30,7 +30,6 @@ namespace fce {
 static __device__ __attribute__((aligned(16))) _Float16 g_dc_zero[8];
 
 constexpr int dc_max(int a, int b) { return a > b ? a : b; }
-constexpr int dc_min(int a, int b) { return a < b ? a : b; }
 
 // compile-time geometry of one instantiation (LDS offsets in 16-byte units)
 template <int C0, int C3, int NCLS, int TH, int TW, int NW>
@@ -65,15 +64,9 @@ struct DcG {
   static constexpr size_t LDS = size_t(TOTAL) * 16;
   static constexpr int NXE = (XR * K0 + NT - 1) / NT;  // x chunks per thread
   static constexpr int NPG3 = NT / K3;                // dw2 position groups (threads >= NPG3 * K3 idle there)
-  // column runs (dc_dw_run): threads = segment x column x chunk (chunk fastest), each streaming the rows of one
-  // segment; segments of two rows at least
-  static constexpr int SG1 = dc_min(NT / (RW * K0), dc_max(1, (TH + 2) / 2)), MR1 = (TH + 2 + SG1 - 1) / SG1;
-  static constexpr int SG2 = dc_min(NT / (TW * K3), dc_max(1, TH / 2)), MR2 = (TH + SG2 - 1) / SG2;
-  static constexpr bool RUN = MR1 <= 4 && MR2 <= 4 && MR1 * SG1 >= TH + 2 && MR2 * SG2 >= TH;  // runs of up to 4
   // blocks per CU the LDS allows (two only under 80 KiB): the register budget follows (one 4-wave block: 512)
   static constexpr int MINB = (LDS <= 80 * 1024 && NW == 4) ? 2 : 1;
-  static_assert(C0 % 8 == 0 && C3 % 8 == 0 && NT % K0 == 0 && NPG3 > 0 && SG1 > 0 && SG2 > 0,
-                "detect cls fused: channel alignment");
+  static_assert(C0 % 8 == 0 && C3 % 8 == 0 && NT % K0 == 0 && NPG3 > 0, "detect cls fused: channel alignment");
 };
 
 struct DclsArgs {
@@ -87,8 +80,7 @@ struct DclsArgs {
   float* pred;
   unsigned long long* best;
   int A, a0;
-  int diag;   // FCE_DCLS_DIAG: block 0 prints its per-stage clocks
-  int dwrun;  // depthwise stages as column runs (dc_dw_run); FCE_DCLS_DWRUN=0: one position per thread (dc_dw)
+  int diag;  // FCE_DCLS_DIAG: block 0 prints its per-stage clocks
 };
 
 __device__ __forceinline__ void dc_tile(const DclsArgs& a, int TH, int TW, int t, int& n, int& y0, int& x0) {
@@ -131,89 +123,6 @@ __device__ __forceinline__ h8 dc_dw(const f4* img, int plane, int p00, int rw, i
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (_Float16)fpin(silu(acc[j >> 1][j & 1]));
   return o;
-}
-
-// the same depthwise 3x3 over a vertical run of MR output positions (one column, four channels: one plane of a
-// chunk): the input rows streamed top to bottom, each 3-tap row read from LDS once and applied to the (up to three)
-// outputs that use it.  Row j feeds output q with ky = j - q, so every output still takes its taps in (ky, kx) order
-// from acc = bias, rows outside the image skipped: the same fmas in the same order as dc_dw, with 3 (MR + 2) row reads
-// for MR outputs instead of 9 MR (img: the first output's top-left tap of this lane's chunk; iy0: its image row).
-// Half a chunk per call keeps the run's accumulators and taps within two waves per SIMD's registers.
-template <int MR, int RW, int K>
-__device__ __forceinline__ void dc_dw_run(const f4* img, int iy0, int H, const float (&wk)[9][4], const float (&bz)[4],
-                                          h4 (&o)[MR]) {
-  f2 acc[MR][2];
-#pragma unroll
-  for (int q = 0; q < MR; ++q) {
-    acc[q][0] = f2{bz[0], bz[1]};
-    acc[q][1] = f2{bz[2], bz[3]};
-  }
-  // rows read one ahead of their fmas, no further (every row's reads hoisted spilled), at constant offsets
-  f4 rv[2][3];
-  auto rd = [&](int j, f4 (&v)[3]) {
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) v[kx] = img[(j * RW + kx) * K];
-  };
-  rd(0, rv[0]);
-#pragma unroll
-  for (int j = 0; j < MR + 2; ++j) {
-    if (j + 1 < MR + 2) rd(j + 1, rv[(j + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);
-    const int yy = iy0 - 1 + j;
-    if (yy >= 0 && yy < H) {
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const f4 v = rv[j & 1][kx];
-#pragma unroll
-        for (int q = 0; q < MR; ++q) {
-          const int ky = j - q;
-          if (ky < 0 || ky > 2) continue;
-          const float* w = wk[ky * 3 + kx];
-          acc[q][0] = __builtin_elementwise_fma(f2{v[0], v[1]}, f2{w[0], w[1]}, acc[q][0]);
-          acc[q][1] = __builtin_elementwise_fma(f2{v[2], v[3]}, f2{w[2], w[3]}, acc[q][1]);
-        }
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int q = 0; q < MR; ++q)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[q][j] = (_Float16)fpin(silu(acc[q][j >> 1][j & 1]));
-}
-
-// the 9 x 4 depthwise weights and 4 biases of channels ch * 8 + 4 hf .. + 3 from the LDS tables ([9][c] fp32)
-__device__ __forceinline__ void dc_weights_half(const float* tab, int c, int ch, int hf, const float* bias,
-                                                float (&wk)[9][4], float (&bz)[4]) {
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const f4 w = *reinterpret_cast<const f4*>(tab + t * c + ch * 8 + hf * 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wk[t][j] = w[j];
-  }
-  const f4 b = *reinterpret_cast<const f4*>(bias + ch * 8 + hf * 4);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bz[j] = b[j];
-}
-
-// one column run of 8 channels: the low plane's four, then the high plane's (img: the run's first tap, low plane)
-template <int MR, int RW, int K>
-__device__ __forceinline__ void dc_dw_run8(const f4* img, int plane, int ch, int iy0, int H, const float* tab, int c,
-                                           const float* bias, h8 (&o)[MR]) {
-  h4 lo[MR];
-  {
-    float wk[9][4], bz[4];
-    dc_weights_half(tab, c, ch, 0, bias, wk, bz);
-    dc_dw_run<MR, RW, K>(img, iy0, H, wk, bz, lo);
-  }
-  h4 hi[MR];
-  {
-    float wk[9][4], bz[4];
-    dc_weights_half(tab, c, ch, 1, bias, wk, bz);
-    dc_dw_run<MR, RW, K>(img + plane, iy0, H, wk, bz, hi);
-  }
-#pragma unroll
-  for (int q = 0; q < MR; ++q) o[q] = h8{lo[q][0], lo[q][1], lo[q][2], lo[q][3], hi[q][0], hi[q][1], hi[q][2], hi[q][3]};
 }
 
 // the 9 x 8 depthwise weights and 8 biases of chunk ch from the LDS tables ([9][c] fp32)
@@ -318,26 +227,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
     stage_barrier();
     tick(1);
     // ---------------- t1 = SiLU(dw1(x)) over the tile + 1-pixel halo -> P
-    // an opaque zero per tile: the runs' weight reads stay in the loop (hoisted out of it, hipcc kept them in scratch)
-    int wz = 0;
-    asm volatile("" : "+s"(wz));
-    if (G::RUN && a.dwrun) {
-      // segments of MR1 rows, the last one moved up to end at the region's last row (its overlap recomputed: the
-      // same values stored twice)
-      const int ch = tid % G::K0, c = (tid / G::K0) % G::RW, sg = tid / (G::K0 * G::RW);
-      if (sg < G::SG1) {
-        const int r0 = min(sg * G::MR1, TH + 2 - G::MR1);
-        const int iy0 = y0 - 1 + r0, ix = x0 - 1 + c;
-        h8 o[G::MR1];
-        dc_dw_run8<G::MR1, G::XW, G::K0>(Qf + (r0 * G::XW + c) * G::K0 + ch, G::QX, ch, iy0, a.H, dwt + wz, C0,
-                                         bias + G::BD1 + wz, o);
-#pragma unroll
-        for (int q = 0; q < G::MR1; ++q) {
-          const bool in = iy0 + q >= 0 && iy0 + q < a.H && ix >= 0 && ix < a.W;
-          P[((r0 + q) * G::RW + c) * G::s1 + ch] = in ? o[q] : zero8;  // outside the image: unused (pw1 zeroes t2)
-        }
-      }
-    } else {
+    {
       const int ch = tid % G::K0;
       float wk[9][8], bz[8];
       dc_weights(dwt, C0, ch, bias + G::BD1, wk, bz);
@@ -378,18 +268,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
     stage_barrier();
     tick(3);
     // ---------------- t3 = SiLU(dw2(t2)) over the tile -> P
-    if (G::RUN && a.dwrun) {
-      const int ch = tid % G::K3, c = (tid / G::K3) % TW, sg = tid / (G::K3 * TW);
-      if (sg < G::SG2) {
-        const int r0 = min(sg * G::MR2, TH - G::MR2);
-        const int iy0 = y0 + r0, ix = x0 + c;
-        h8 o[G::MR2];
-        dc_dw_run8<G::MR2, G::RW, G::K3>(Qf + (r0 * G::RW + c) * G::K3 + ch, G::QT, ch, iy0, a.H, dwt + 9 * C0 + wz, C3,
-                                         bias + G::BD2 + wz, o);
-#pragma unroll
-        for (int q = 0; q < G::MR2; ++q) P[((r0 + q) * TW + c) * G::s3 + ch] = iy0 + q < a.H && ix < a.W ? o[q] : zero8;
-      }
-    } else if (tid < G::NPG3 * G::K3) {
+    if (tid < G::NPG3 * G::K3) {
       const int ch = tid % G::K3;
       float wk[9][8], bz[8];
       dc_weights(dwt + 9 * C0, C3, ch, bias + G::BD2, wk, bz);
@@ -487,9 +366,7 @@ __global__ __launch_bounds__(NW * 64, (DcG<C0, C3, NCLS, TH, TW, NW>::MINB)) voi
 // 8 x 16 tiles with 8 waves (~103 KiB LDS, one block per CU), P4 8 x 8 with 8 waves (~122 KiB); P5 (c0 256) needs
 // > 160 KiB at any tile of 64 positions and keeps the five ops.  The kernel is bound by its VALU (the depthwise
 // FMAs and the SiLU / sigmoid of every stage, recomputed over the 1-pixel halo for dw1 / pw1) at two waves per SIMD
-// (FCE_DCLS_DIAG stage clocks).  The depthwise stages run as column runs (dc_dw_run: each input row read
-// from LDS once per run instead of once per output): P3 92.2-94.4 -> 88.6-91.6 us, P4 47.8-48.0 -> 46.1-47.4, dw2's
-// clocks 5.2k -> 4.6k per tile, dw1's unchanged (its SiLUs, not its reads, bound it; profiles/r06as_dcls_dwrun.txt).
+// (FCE_DCLS_DIAG stage clocks).
 struct DcInst {
   int c0, c3, nc;
 };
@@ -584,8 +461,6 @@ int detect_cls_fused(const fce_dcls_desc& d, const fce_tensor& x, const fce_dete
   {
     const char* de = getenv("FCE_DCLS_DIAG");
     a.diag = de && atoi(de) != 0;
-    const char* dr = getenv("FCE_DCLS_DWRUN");  // A/B: 0 = one position per thread
-    a.dwrun = !(dr && *dr && atoi(dr) == 0);
   }
   return dc_dispatch(inst, a, x.n, s);
 }
