@@ -449,17 +449,23 @@ struct Dring3Geom {
 static constexpr bool dring3_fits(int s, int rp, int nch, int nbuf, int cpw = 1, int sub = 1) {
   return size_t(nbuf) * ((((((cpw * rp * sub - 1) * s + 3) * (15 * s + 3) * 4 * nch + 63) / 64 + 3) / 4) * 4 * 64) * 16 <=
              80 * 1024 &&       // two blocks per CU
-         (cpw == 1 || nch == 1) &&               // two cout tiles of 64-channel A fragments spill at two waves
-         (rp < 8 || (nch == 1 && nbuf == 3)) &&  // per SIMD, and so do 8-row tiles of them (or with four buffers)
-         (nch < 4 || (s == 2 && rp == 1)) &&  // 128 channels (36 A fragments in registers): stride-2 one-row tiles
-         (sub == 1 || (sub == 2 && rp * sub <= 8));  // only; the two-row stride-1 ones spilled (31.2 against 24.3 us,
-}                                                    // r06al); sub-tiles: 8 rows of held residuals at most
+         // two cout tiles of 64-channel A fragments: 1- and 2-row tiles with three buffers only (253 VGPRs at 2 rows;
+         // more rows or buffers spill at two waves per SIMD)
+         (cpw == 1 || nch == 1 || (nch == 2 && rp <= 2 && nbuf == 3 && sub == 1)) &&
+         (rp < 8 || (nch == 1 && nbuf == 3)) &&  // 8-row tiles of 64-channel fragments spill too (or with four buffers)
+         // 128 channels (36 A fragments in registers): stride-2 one-row tiles only; the two-row stride-1 ones spilled
+         // (31.2 against 24.3 us, r06al)
+         (nch < 4 || (s == 2 && rp == 1)) &&
+         (sub == 1 || (sub == 2 && rp * sub <= 8));  // sub-tiles: 8 rows of held residuals at most
+}
 // the candidates offered: two buffers or one-row tiles only for the 128-channel tiles, which need them to fit (at 32 /
-// 64 channels the two-buffer ones are the big stride-2 tiles, which spill); two sub-tiles only for the 32-channel
+// 64 channels the two-buffer ones are the big stride-2 tiles, which spill), and for the 64-channel two-cout-tile ones
+// (0xd19: 2 x 1 rows per block; 0xd29 25.6 against 25.9-26.3 us for 0xd41 at 64 -> 64 80 x 80, its MFMA phase 1.97k
+// against 2.16k clocks per tile at half the LDS reads, r06av); two sub-tiles only for the 32-channel
 // stride-1 convs, the one place they measured ahead (48.4 against 49.9 us at 160 x 160; 64 -> 64 at 80 x 80 and the
 // stride-2 ones slower, the 64-channel 8-row tiles spilling: profiles/r06_dring_probe.txt)
 static constexpr bool dring3_offer(int s, int rp, int nch, int nbuf, int cpw = 1, int sub = 1) {
-  return dring3_fits(s, rp, nch, nbuf, cpw, sub) && (nch == 4 || (nbuf > 2 && rp > 1)) &&
+  return dring3_fits(s, rp, nch, nbuf, cpw, sub) && (nch == 4 || (nbuf > 2 && (rp > 1 || (cpw == 2 && nch == 2)))) &&
          (nbuf > 2 || !dring3_fits(s, rp, nch, 3, cpw, sub)) && (sub == 1 || (nbuf > 2 && rp >= 2 && nch == 1 && s == 1));
 }
 int launch_dring3(const ConvArgs& a, int rp, int nbuf, int cpw, int sub, int stride, hipStream_t s);
